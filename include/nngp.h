@@ -1,0 +1,166 @@
+/*
+ * nngp.h -- C-ABI of libnngp_hip.so, the MI355X (gfx950) hot path of nnGParareal.
+ *
+ * The reference (Python + jax, /root/reference) has no native code: its hot path is three
+ * duck-typed Python plugin calls that a process pool fans out:
+ *
+ *   1. propagator  SolverAbstr.run_F/run_G(t0, t1, u0) -> u1      solver.py:29-69, 86-107
+ *                  (Parareal fans run_F over slices: parareal.py:310-315)
+ *   2. model       NNGP_p.predict(new_x, ...) -> preds[d]          models.py:171-226
+ *                  (kNN :177-179, n*9*R Nelder-Mead fits of the -LML :185-202, 228-260,
+ *                   argmin :207-215, posterior mean :162-168, 217)
+ *   3. executor    pool.map(fn, *iterables)                        parareal.py:16-24, 58-64
+ *
+ * Each entry point below replaces one of those call sites with ONE stream-ordered launch
+ * sequence on the GPU.  Python binds them through ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - All array arguments are DEVICE pointers (hipMalloc / torch.cuda memory) unless the
+ *     parameter name ends in `_host`.  Layouts are row-major: states are [n_slices][d], which
+ *     is exactly the reference's u[i, :, k] slice for consecutive i.
+ *   - Every call is asynchronous on `stream` (a hipStream_t; NULL = default stream) and
+ *     returns 0 on success, a negative NNGP_E_* code otherwise; nngp_last_error() gives a
+ *     thread-local message.  Nothing here allocates per call except the library's own
+ *     grow-only device workspace (nngp_predict), so steady-state calls never hit hipMalloc.
+ *   - Arithmetic is IEEE fp64 throughout (the reference runs jax with x64 enabled,
+ *     e.g. models.py:8, RK.py:13).  Kernels are built with -ffp-contract=off so that every
+ *     add/mul rounds exactly where the reference's does.
+ */
+#ifndef NNGP_H_
+#define NNGP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NNGP_ABI_VERSION 1
+
+/* error codes */
+#define NNGP_OK 0
+#define NNGP_E_ARG (-1)       /* invalid argument (shape, enum, null pointer)            */
+#define NNGP_E_HIP (-2)       /* a HIP runtime call failed                               */
+#define NNGP_E_UNSUPPORTED (-3) /* valid in the reference but not (yet) on this path     */
+
+/* Vector fields.  Reference: systems.py (modern) and new_lib.Systems (legacy twin). */
+enum nngp_system_kind {
+    NNGP_SYS_LORENZ = 0,            /* systems.py:225-247                                  */
+    NNGP_SYS_HOPF = 1,              /* systems.py:140-172 (non-autonomous Hopf), param[0]=maxtime */
+    NNGP_SYS_THOMAS_LABYRINTH = 2,  /* systems.py:250-288                                  */
+    NNGP_SYS_FHN_ODE = 3,           /* systems.py:80-106                                   */
+    NNGP_SYS_ROSSLER = 4,           /* systems.py:109-137                                  */
+    NNGP_SYS_BRUSSELATOR = 5,       /* systems.py:202-222                                  */
+    NNGP_SYS_DBL_PEND = 6,          /* systems.py:175-199                                  */
+    NNGP_SYS_BURGERS = 7,           /* systems.py:402-459, nx = d, param[0] = nu           */
+    NNGP_SYS_FHN_PDE = 8            /* systems.py:291-398, nx = d_x, d = 2*d_x*d_x         */
+};
+
+/* Explicit Runge-Kutta tableaux, RK.py:30-48 (value = order). */
+enum nngp_tableau { NNGP_RK1 = 1, NNGP_RK2 = 2, NNGP_RK4 = 4, NNGP_RK8 = 8 };
+
+/* Step-size convention.
+ *   FIXED:    h = (t1 - t0)/steps for every step          RK.run_get_last, RK.py:101-109
+ *   LINSPACE: h_n = t[n+1] - t[n], t = np.linspace(t0, t1, steps+1)
+ *             RK.run / legacy new_lib.RK (RK.py:91-99, new_lib.py:87-137) -- the convention
+ *             of every published scalability run.                                            */
+enum nngp_step_mode { NNGP_STEP_FIXED = 0, NNGP_STEP_LINSPACE = 1 };
+
+/* One ODE/PDE right-hand side, optionally wrapped by the '-11' normalisation of
+ * ODE.get_vector_field (systems.py:32-44, utils.py:14-33):
+ *     f_n(u) = f((u+1)/2*(mx-mn) + mn) * (2/(mx-mn))                                       */
+typedef struct nngp_system {
+    int32_t kind;        /* enum nngp_system_kind                                         */
+    int32_t d;           /* state dimension                                               */
+    int32_t nx;          /* grid points per axis (Burgers: d; FHN_PDE: d_x); else 0        */
+    int32_t normalized;  /* 0: identity, 1: '-11' wrapper                                 */
+    double param[4];     /* HOPF: [0]=maxtime (tspan[1]); BURGERS: [0]=nu; else unused     */
+    const double *norm;  /* DEVICE [3*d] = mn | (mx-mn) | 2/(mx-mn), or NULL if identity   */
+} nngp_system;
+
+/* ---- library ---------------------------------------------------------------------------- */
+int nngp_abi_version(void);
+const char *nngp_last_error(void);
+/* Number of visible HIP devices (0 when no GPU); never fails. */
+int nngp_device_count(void);
+
+/* ---- 1. fine / coarse propagator --------------------------------------------------------
+ * Replaces: SolverRK.run_F / run_G for every slice of one Parareal iteration
+ *           (solver.py:86-107 via RK.run_get_last RK.py:101-109 / _RK_jax_last RK.py:146-174),
+ *           as fanned out by pool.map(solver.run_F_timed, ...) at parareal.py:310-315, and the
+ *           legacy RK_last (new_lib.py:57-69, 939-945).
+ * Integrates n_slices independent initial values u0[i] from t0[i] to t1[i] with `steps`
+ * steps of tableau `tableau`; writes the end states to uF[i].  The paging quirk of
+ * solver.py:86-99 is a host-side loop over pages calling this once per page.
+ * t0, t1: DEVICE [n_slices]; u0, uF: DEVICE [n_slices][sys->d]; uF may alias u0.          */
+int nngp_rk_batch(const nngp_system *sys, int tableau, int step_mode, int n_slices,
+                  const double *t0, const double *t1, int64_t steps, const double *u0,
+                  double *uF, void *stream);
+
+/* Legacy global-grid variant (the legacy driver's initial coarse sweep, new_lib.py:902-906,
+ * integrates ONE np.linspace(g0, g1, gsteps+1) grid and sub-samples it at slice boundaries).
+ * Slice i performs grid steps j0[i] .. j0[i]+steps-1 of the grid (g0[i], g1[i], gsteps):
+ * t[j] = j*((g1-g0)/gsteps) + g0, t[gsteps] = g1, h = t[j+1]-t[j].  j0: DEVICE int64 [n].  */
+int nngp_rk_batch_grid(const nngp_system *sys, int tableau, int n_slices, const double *g0,
+                       const double *g1, int64_t gsteps, const int64_t *j0, int64_t steps,
+                       const double *u0, double *uF, void *stream);
+
+/* Vector field evaluation f_n(u) for n states (what ODE.get_vector_field() returns as a
+ * callable, systems.py:32-44).  u, out: DEVICE [n][sys->d].                                 */
+int nngp_rhs_batch(const nngp_system *sys, int n, const double *u, double *out, void *stream);
+
+/* Elementwise  out = (a - b) + c   (c may be NULL: out = a - b), n doubles, DEVICE.
+ *   Parareal update with the classic model: u = (uF_prev - uG_prev) + uG_new
+ *   (models.py:82-83 + parareal.py:382); training targets D = uF - uG (parareal.py:337).     */
+int nngp_parareal_update(int64_t n, const double *a, const double *b, const double *c,
+                         double *out, void *stream);
+
+/* ---- 2. nnGP correction -----------------------------------------------------------------
+ * kNN (models.py:177-179): indices of the m rows of X[rows][d] nearest to q[d] in squared
+ * euclidean distance, ascending, ties broken by row index.  idx_out: DEVICE int32 [m];
+ * dist_out: DEVICE [m] or NULL.  Requires 1 <= m <= rows.                                   */
+int nngp_knn(const double *X, int64_t rows, int d, const double *q, int m, int32_t *idx_out,
+             double *dist_out, void *stream);
+
+/* Batched hyper-parameter fits, replacing pool.map(NNGP_p._get_opt_par, ...) at
+ * models.py:197-202 -> opt_theta (models.py:254-260) -> scipy Nelder-Mead on log_lik
+ * (models.py:240-252).  Fit f minimises -LML(theta | xm, ym[:, coord[f]], 10**jitter) with
+ * jitter = jitter_exp_host[jitter_idx[f]], starting from theta0[f], by the rules of scipy's
+ * _minimize_neldermead (rho=1, chi=2, psi=0.5, sigma=0.5, 5% initial simplex, xatol/fatol stop,
+ * maxiter = maxfev).  A NaN -LML (failed Cholesky) counts as +inf (models.py:250-251).
+ *   xm, ym: DEVICE [m][d]; coord, jitter_idx: DEVICE int32 [n_fits]; theta0: DEVICE [n_fits][2];
+ *   jitter_exp_host: HOST [n_jitter] exponents (e.g. -20..-12, models.py:186);
+ *   theta_out: DEVICE [n_fits][2]; fval_out: DEVICE [n_fits]; nfev_out: DEVICE int32 or NULL.
+ * Requires 1 <= m <= 32.                                                                   */
+int nngp_nm_fit_batch(int m, int d, const double *xm, const double *ym, int n_fits,
+                      const int32_t *coord, const int32_t *jitter_idx, int n_jitter,
+                      const double *jitter_exp_host, const double *theta0, double fatol,
+                      double xatol, int maxfev, double *theta_out, double *fval_out,
+                      int32_t *nfev_out, void *stream);
+
+/* Posterior mean K(xm, new_x)^T alpha per coordinate c with hyper-parameters theta[c] and
+ * jitter 10**jitter_exp_host[jitter_idx[c]] (models.py:162-168, 217).  NaN if the Cholesky
+ * fails (jax semantics).  theta: DEVICE [d][2]; jitter_idx: DEVICE int32 [d]; out: DEVICE [d]. */
+int nngp_gp_mean(int m, int d, const double *xm, const double *ym, const double *new_x,
+                 const double *theta, const int32_t *jitter_idx, int n_jitter,
+                 const double *jitter_exp_host, double *out, void *stream);
+
+/* One full correction for one slice = NNGP_p.predict (models.py:171-226) fused:
+ * kNN over the training set X/Y[rows][d] at new_x[d], d*n_jitter*n_restarts fits in the
+ * reference's product(coord, jitter, restart) order (models.py:186-192) starting from
+ * theta0[d*n_jitter*n_restarts][2] (the host replays rng.integers(-8, 0, 2) in that order),
+ * per-coordinate first-argmin of fval (models.py:207-215) and the posterior mean.
+ *   preds_out = mean;  if bias != NULL also out = preds + bias (parareal.py:382).
+ *   fits_out: DEVICE [n_fits][4] = (theta_x, theta_y, fval, nfev) or NULL.
+ *   jitter_exp_host: HOST [n_jitter]. All other arrays DEVICE.  Requires 1 <= m <= 32.   */
+int nngp_predict(const double *X, const double *Y, int64_t rows, int d, const double *new_x,
+                 int m, int n_jitter, const double *jitter_exp_host, int n_restarts,
+                 const double *theta0, double fatol, double xatol, int maxfev,
+                 double *preds_out, const double *bias, double *out, double *fits_out,
+                 void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NNGP_H_ */

@@ -1,0 +1,99 @@
+"""ctypes binding of libnngp_hip.so (include/nngp.h).
+
+The product path has NO CPU fallback: if the HIP library is missing or no GPU is visible,
+every compute entry point raises.  `lib()` loads the in-tree build
+(nearest-neighbors-gparareal_amd/lib/libnngp_hip.so, produced by csrc/Makefile).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'lib', 'libnngp_hip.so')
+CSRC = os.path.join(HERE, 'csrc')
+
+# enums (include/nngp.h)
+SYS_LORENZ, SYS_HOPF, SYS_THOMAS_LABYRINTH, SYS_FHN_ODE, SYS_ROSSLER = 0, 1, 2, 3, 4
+SYS_BRUSSELATOR, SYS_DBL_PEND, SYS_BURGERS, SYS_FHN_PDE = 5, 6, 7, 8
+TABLEAU = {'RK1': 1, 'RK2': 2, 'RK4': 4, 'RK8': 8}
+STEP_FIXED, STEP_LINSPACE = 0, 1
+
+EXPORTS = ['nngp_abi_version', 'nngp_last_error', 'nngp_device_count', 'nngp_rk_batch', 'nngp_rk_batch_grid',
+           'nngp_rhs_batch', 'nngp_parareal_update', 'nngp_knn', 'nngp_nm_fit_batch',
+           'nngp_gp_mean', 'nngp_predict']
+
+
+class NNGPError(RuntimeError):
+    pass
+
+
+class CSystem(ctypes.Structure):
+    """struct nngp_system"""
+    _fields_ = [('kind', ctypes.c_int32), ('d', ctypes.c_int32), ('nx', ctypes.c_int32),
+                ('normalized', ctypes.c_int32), ('param', ctypes.c_double * 4),
+                ('norm', ctypes.c_void_p)]
+
+
+_lib = None
+_vp = ctypes.c_void_p
+_dp = ctypes.POINTER(ctypes.c_double)
+
+
+def build(force=False):
+    """Compile csrc/ for gfx950 (hipcc cross-compiles without a GPU)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(['make', '-s', '-j3', '-C', CSRC], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NNGPError(f'HIP library not built: {LIB_PATH} missing (run __graft_entry__.build() or '
+                        f'make -C {CSRC}); there is no CPU fallback')
+    L = ctypes.CDLL(LIB_PATH)
+    i32, i64, dbl = ctypes.c_int, ctypes.c_int64, ctypes.c_double
+    L.nngp_abi_version.restype = i32
+    L.nngp_last_error.restype = ctypes.c_char_p
+    L.nngp_device_count.restype = i32
+    L.nngp_rk_batch.argtypes = [ctypes.POINTER(CSystem), i32, i32, i32, _vp, _vp, i64, _vp, _vp, _vp]
+    L.nngp_rk_batch_grid.argtypes = [ctypes.POINTER(CSystem), i32, i32, _vp, _vp, i64, _vp, i64, _vp, _vp, _vp]
+    L.nngp_rhs_batch.argtypes = [ctypes.POINTER(CSystem), i32, _vp, _vp, _vp]
+    L.nngp_parareal_update.argtypes = [i64, _vp, _vp, _vp, _vp, _vp]
+    L.nngp_knn.argtypes = [_vp, i64, i32, _vp, i32, _vp, _vp, _vp]
+    L.nngp_nm_fit_batch.argtypes = [i32, i32, _vp, _vp, i32, _vp, _vp, i32, _dp, _vp, dbl, dbl, i32,
+                                    _vp, _vp, _vp, _vp]
+    L.nngp_gp_mean.argtypes = [i32, i32, _vp, _vp, _vp, _vp, _vp, i32, _dp, _vp, _vp]
+    L.nngp_predict.argtypes = [_vp, _vp, i64, i32, _vp, i32, i32, _dp, i32, _vp, dbl, dbl, i32, _vp,
+                               _vp, _vp, _vp, _vp]
+    for name in EXPORTS:
+        if name not in ('nngp_abi_version', 'nngp_last_error', 'nngp_device_count'):
+            getattr(L, name).restype = i32
+    if L.nngp_abi_version() != 1:
+        raise NNGPError('ABI version mismatch')
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().nngp_last_error().decode(errors='replace')
+        raise NNGPError(f'libnngp_hip error {rc}: {msg}')
+
+
+def host_doubles(a):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a, a.ctypes.data_as(_dp)
+
+
+def require_gpu():
+    """The product path runs on the GPU only; fail loudly otherwise."""
+    import torch
+    if not torch.cuda.is_available():
+        raise NNGPError('no HIP device visible: nnGParareal-amd has no CPU fallback')
+    lib()
+    return torch

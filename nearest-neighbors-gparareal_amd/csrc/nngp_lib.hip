@@ -1,0 +1,65 @@
+// nngp_lib.hip -- library-level entry points: version, errors, device count, workspace.
+#include <stdarg.h>
+
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+
+namespace nngp {
+
+static thread_local char g_err[1024] = "";
+
+void set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+struct Ws {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+static std::vector<Ws> g_ws;
+static std::mutex g_ws_mu;
+
+void *workspace(size_t bytes, int *err) {
+    int dev = 0;
+    *err = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        set_error("hipGetDevice failed");
+        *err = NNGP_E_HIP;
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    if ((int)g_ws.size() <= dev) g_ws.resize(dev + 1);
+    Ws &w = g_ws[dev];
+    if (w.bytes < bytes) {
+        // grow (x1.5) -- the stream-ordered users are synchronised by hipFree's implicit sync
+        if (w.ptr) (void)hipFree(w.ptr);
+        size_t nb = bytes + bytes / 2 + 4096;
+        hipError_t e = hipMalloc(&w.ptr, nb);
+        if (e != hipSuccess) {
+            w.ptr = nullptr;
+            w.bytes = 0;
+            set_error("hipMalloc(%zu) for workspace failed: %s", nb, hipGetErrorString(e));
+            *err = NNGP_E_HIP;
+            return nullptr;
+        }
+        w.bytes = nb;
+    }
+    return w.ptr;
+}
+
+}  // namespace nngp
+
+extern "C" int nngp_abi_version(void) { return NNGP_ABI_VERSION; }
+
+extern "C" const char *nngp_last_error(void) { return nngp::g_err; }
+
+extern "C" int nngp_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}

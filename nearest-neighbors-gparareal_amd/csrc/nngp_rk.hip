@@ -1,0 +1,635 @@
+// nngp_rk.hip -- batched fine/coarse Runge-Kutta propagator for gfx950 (MI355X).
+//
+// Replaces the reference's per-slice fine solve SolverRK.run_F -> RK.run_get_last ->
+// _RK_jax_last (solver.py:86-107, RK.py:101-109, 146-174), fanned over the unconverged slices by
+// pool.map at parareal.py:310-315 (legacy: RK_last / RK_jax_, new_lib.py:57-137, 939-945).
+//
+// One launch integrates ALL slices of one Parareal iteration.  Two kernel shapes:
+//   * lane kernel  (ODEs, d <= 4): one lane = one slice, state + all S stage vectors in VGPRs,
+//     no LDS, no barriers.  The RHS is a handful of dependent fp64 ops, so a slice is a serial
+//     chain of 10^3..10^9 RK steps: this shape is latency-bound by construction.
+//   * field kernel (Burgers d=nx, FHN-PDE d=2 nx^2): one workgroup = one slice, thread t owns
+//     elements t, t+BT, ... (EPT per thread, u and the S stage vectors in VGPRs).  The stage input
+//     is staged (already inverse-normalised) in a double-buffered LDS image so the stencil reads
+//     neighbours from LDS; exactly one __syncthreads per stage.
+// HBM traffic is 16*d bytes per slice per launch (read u0, write uF); everything else stays on
+// chip, so the roofline is FP64 VALU, not HBM.
+//
+// Numerics: compiled with -ffp-contract=off; every add/mul is rounded in the order of the
+// reference expression it restates (cited inline).  Zero tableau entries are skipped at compile
+// time, which is exact for finite stages (t + 0*k == t).
+
+#include <algorithm>
+
+#include "common.h"
+#include "tableau.h"
+
+namespace nngp {
+
+// ---------------------------------------------------------------------------------------------
+// ODE right-hand sides (systems.py), one lane = one state
+// ---------------------------------------------------------------------------------------------
+struct LaneArgs {
+    double mn[4], w[4], sc[4];   // '-11' wrapper: mn, (mx-mn), 2/(mx-mn)   (utils.py:14-33)
+    double param[4];
+    int normalized;
+    const double *norm;          // device [3D], loaded into the fields above by each lane
+};
+
+template <int SYS> struct LaneSys;
+
+template <> struct LaneSys<NNGP_SYS_LORENZ> {   // systems.py:232-238
+    static constexpr int D = 3;
+    __device__ static void f(const double *u, double *o, const LaneArgs &) {
+        o[0] = 10 * (u[1] - u[0]);
+        o[1] = (28 * u[0] - u[1]) - u[0] * u[2];
+        o[2] = u[0] * u[1] - (8.0 / 3) * u[2];
+    }
+};
+template <> struct LaneSys<NNGP_SYS_HOPF> {     // systems.py:148-154
+    static constexpr int D = 3;
+    __device__ static void f(const double *u, double *o, const LaneArgs &a) {
+        const double g = ((u[2] / a.param[0]) - u[0] * u[0]) - u[1] * u[1];
+        o[0] = -u[1] + u[0] * g;
+        o[1] = u[0] + u[1] * g;
+        o[2] = 1.0;
+    }
+};
+template <> struct LaneSys<NNGP_SYS_THOMAS_LABYRINTH> {   // systems.py:257-271
+    static constexpr int D = 3;
+    __device__ static void f(const double *u, double *o, const LaneArgs &) {
+        o[0] = -0.5 * u[0] + 10.0 * sin(u[1]);
+        o[1] = -0.5 * u[1] + 10.0 * sin(u[2]);
+        o[2] = -0.5 * u[2] + 10.0 * sin(u[0]);
+    }
+};
+template <> struct LaneSys<NNGP_SYS_FHN_ODE> {  // systems.py:87-95 (u**3 = u*(u*u), jax)
+    static constexpr int D = 2;
+    __device__ static void f(const double *u, double *o, const LaneArgs &) {
+        const double c = 3;
+        o[0] = c * ((u[0] - ((u[0] * (u[0] * u[0])) / 3)) + u[1]);
+        o[1] = -(1 / c) * ((u[0] - 0.2) + 0.2 * u[1]);
+    }
+};
+template <> struct LaneSys<NNGP_SYS_ROSSLER> {  // systems.py:116-125
+    static constexpr int D = 3;
+    __device__ static void f(const double *u, double *o, const LaneArgs &) {
+        o[0] = -u[1] - u[2];
+        o[1] = u[0] + (0.2 * u[1]);
+        o[2] = 0.2 + u[2] * (u[0] - 5.7);
+    }
+};
+template <> struct LaneSys<NNGP_SYS_BRUSSELATOR> {  // systems.py:209-214
+    static constexpr int D = 2;
+    __device__ static void f(const double *u, double *o, const LaneArgs &) {
+        o[0] = (1 + (u[0] * u[0]) * u[1]) - (3 + 1) * u[0];
+        o[1] = 3 * u[0] - (u[0] * u[0]) * u[1];
+    }
+};
+template <> struct LaneSys<NNGP_SYS_DBL_PEND> {  // systems.py:182-189
+    static constexpr int D = 4;
+    __device__ static void f(const double *u, double *o, const LaneArgs &) {
+        const double c = cos(u[0] - u[2]), s = sin(u[0] - u[2]);
+        const double pre = -1 / (2 - c * c);
+        o[0] = u[1];
+        o[1] = pre * ((((u[1] * u[1]) * c) * s + (u[3] * u[3]) * s) + 2 * sin(u[0]) - c * sin(u[2]));
+        o[2] = u[3];
+        o[3] = pre * ((((-2 * (u[1] * u[1])) * s - ((u[3] * u[3]) * s) * c) - (2 * c) * sin(u[0])) +
+                      2 * sin(u[2]));
+    }
+};
+
+// f_n(u) = f(inverse(u)) * scale   (systems.py:36-40)
+template <int SYS>
+__device__ __forceinline__ void lane_rhs(const double *u, double *o, const LaneArgs &a) {
+    constexpr int D = LaneSys<SYS>::D;
+    if (a.normalized) {
+        double v[D];
+#pragma unroll
+        for (int c = 0; c < D; c++) v[c] = ((u[c] + 1) / 2) * a.w[c] + a.mn[c];
+        LaneSys<SYS>::f(v, o, a);
+#pragma unroll
+        for (int c = 0; c < D; c++) o[c] = o[c] * a.sc[c];
+    } else {
+        LaneSys<SYS>::f(u, o, a);
+    }
+}
+
+// FIXED:    h = dt = (t1-t0)/steps (RK.py:103).
+// LINSPACE: step n of slice i is step j = j0 + n of the grid np.linspace(t0, t1, gsteps+1):
+//           t[j] = j*gstep + t0 (gstep = (t1-t0)/gsteps), t[gsteps] = t1, h = t[j+1]-t[j]
+//           (RK.py:91-99, 121; new_lib.py:87-137).  j0 = 0, gsteps = steps is the per-slice grid;
+//           j0 > 0 walks one global grid (the legacy initial coarse sweep, new_lib.py:902-906).
+__device__ __forceinline__ double step_size(bool linspace, int64_t n, int64_t j0, int64_t gsteps,
+                                            double t0, double t1, double dt) {
+    if (!linspace) return dt;
+    const int64_t j = j0 + n;
+    const double tn = (double)j * dt + t0;
+    const double tn1 = (j + 1 == gsteps) ? t1 : (double)(j + 1) * dt + t0;
+    return tn1 - tn;
+}
+
+template <int SYS, int ORDER, bool LINSPACE>
+__global__ void __launch_bounds__(64) rk_lane_kernel(LaneArgs args, int n_slices,
+                                                     const double *__restrict__ t0,
+                                                     const double *__restrict__ t1, int64_t steps,
+                                                     int64_t gsteps, const int64_t *__restrict__ j0s,
+                                                     const double *__restrict__ u0,
+                                                     double *__restrict__ uF) {
+    using T = Tableau<ORDER>;
+    constexpr int S = T::S;
+    constexpr int D = LaneSys<SYS>::D;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_slices) return;
+    if (args.normalized) {
+#pragma unroll
+        for (int c = 0; c < D; c++) {
+            args.mn[c] = args.norm[c];
+            args.w[c] = args.norm[D + c];
+            args.sc[c] = args.norm[2 * D + c];
+        }
+    }
+    double u[D], k[S][D], tmp[D];
+#pragma unroll
+    for (int c = 0; c < D; c++) u[c] = u0[(size_t)i * D + c];
+    const double T0 = t0[i], T1 = t1[i];
+    const double dt = (T1 - T0) / (double)(LINSPACE ? gsteps : steps);
+    const int64_t j0 = j0s ? j0s[i] : 0;
+    for (int64_t n = 0; n < steps; n++) {
+        const double h = step_size(LINSPACE, n, j0, gsteps, T0, T1, dt);
+        // k_0 = h f(u); k_i = h f(u + sum_{j<i} a_ij k_j)     (RK.py:153-170)
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+            if (s == 0) {
+                lane_rhs<SYS>(u, k[0], args);
+            } else {
+#pragma unroll
+                for (int c = 0; c < D; c++) {
+                    double t = 0.0;
+#pragma unroll
+                    for (int j = 0; j < s; j++)
+                        if (T::A[s][j] != 0.0) t = t + T::A[s][j] * k[j][c];
+                    tmp[c] = u[c] + t;
+                }
+                lane_rhs<SYS>(tmp, k[s], args);
+            }
+#pragma unroll
+            for (int c = 0; c < D; c++) k[s][c] = h * k[s][c];
+        }
+        // u + jnp.sum(b*k, 1)  (RK.py:170)
+#pragma unroll
+        for (int c = 0; c < D; c++) {
+            double acc = 0.0;
+            bool first = true;
+#pragma unroll
+            for (int s = 0; s < S; s++) {
+                if (T::B[s] == 0.0) continue;
+                const double v = T::B[s] * k[s][c];
+                acc = first ? v : acc + v;
+                first = false;
+            }
+            u[c] = u[c] + acc;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < D; c++) uF[(size_t)i * D + c] = u[c];
+}
+
+// ---------------------------------------------------------------------------------------------
+// PDE right-hand sides (Burgers, FHN-PDE), one workgroup = one slice
+// ---------------------------------------------------------------------------------------------
+struct FieldArgs {
+    int d, nx, normalized;
+    const double *norm;   // device [3d] = mn | w | sc, or nullptr
+    double c_off, c_diag, c_grad;   // Burgers: nu/dx^2, -2 nu/dx^2, 1/(2dx)
+    double a_off, a_diag, b_off, b_diag;   // FHN-PDE: a*L and b*L entries
+};
+
+// Burgers row i: (Dxx@u)_i - u_i (Dx@u)_i with non-zeros summed in ascending column order
+// (systems.py:421-446)
+__device__ __forceinline__ double burgers_elem(const double *__restrict__ V, int i, int d,
+                                               const FieldArgs &fa) {
+    const double cxx = fa.c_off, cdg = fa.c_diag, q = fa.c_grad;
+    double lap, grad;
+    if (i == 0) {
+        lap = (cdg * V[0] + cxx * V[1]) + cxx * V[d - 1];
+        grad = q * V[1] + (-q) * V[d - 1];
+    } else if (i == d - 1) {
+        lap = (cxx * V[0] + cxx * V[d - 2]) + cdg * V[d - 1];
+        grad = q * V[0] + (-q) * V[d - 2];
+    } else {
+        lap = (cxx * V[i - 1] + cdg * V[i]) + cxx * V[i + 1];
+        grad = (-q) * V[i - 1] + q * V[i + 1];
+    }
+    return lap - V[i] * grad;
+}
+
+// 5-point periodic neighbourhood of grid point p = y*nx + x with its columns in ascending order
+// and a flag for the diagonal slot; precomputed once per element (a 9-comparator sorting
+// network on named registers -- no runtime-indexed arrays, so nothing spills to scratch).
+struct Nbr5 {
+    int c0, c1, c2, c3, c4;
+    bool d0, d1, d2, d3, d4;
+};
+
+__device__ __forceinline__ void cswap(int &a, bool &fa, int &b, bool &fb) {
+    if (a > b) {
+        const int t = a; a = b; b = t;
+        const bool u = fa; fa = fb; fb = u;
+    }
+}
+
+__device__ inline Nbr5 fhn_neighbours(int nx, int p) {
+    const int y = p / nx, x = p - y * nx;
+    const int ym = (y == 0) ? nx - 1 : y - 1, yp = (y == nx - 1) ? 0 : y + 1;
+    const int xm = (x == 0) ? nx - 1 : x - 1, xp = (x == nx - 1) ? 0 : x + 1;
+    Nbr5 r{ym * nx + x, y * nx + xm, p, y * nx + xp, yp * nx + x, false, false, true, false, false};
+    // optimal 5-input sorting network
+    cswap(r.c0, r.d0, r.c1, r.d1); cswap(r.c3, r.d3, r.c4, r.d4);
+    cswap(r.c2, r.d2, r.c4, r.d4); cswap(r.c2, r.d2, r.c3, r.d3);
+    cswap(r.c0, r.d0, r.c3, r.d3); cswap(r.c0, r.d0, r.c2, r.d2);
+    cswap(r.c1, r.d1, r.c4, r.d4); cswap(r.c1, r.d1, r.c3, r.d3);
+    cswap(r.c1, r.d1, r.c2, r.d2);
+    return r;
+}
+
+// ((a L)@v)_p with the 5 terms in ascending column order (systems.py:365-366: `a*(DXX+DYY)@u1`
+// multiplies the matrix by a first)
+__device__ __forceinline__ double fhn_lap(const double *__restrict__ V, const Nbr5 &nb, double off,
+                                          double diag) {
+    double s = (nb.d0 ? diag : off) * V[nb.c0];
+    s = s + (nb.d1 ? diag : off) * V[nb.c1];
+    s = s + (nb.d2 ? diag : off) * V[nb.c2];
+    s = s + (nb.d3 ? diag : off) * V[nb.c3];
+    s = s + (nb.d4 ? diag : off) * V[nb.c4];
+    return s;
+}
+
+// <= 256 threads per slice leaves ~170 VGPRs for u, the S stage vectors and the neighbour table
+template <int SYS, int ORDER, bool LINSPACE, int EPT>
+__global__ void __launch_bounds__(256) rk_field_kernel(FieldArgs fa, int n_slices,
+                                                        const double *__restrict__ t0,
+                                                        const double *__restrict__ t1,
+                                                        int64_t steps, int64_t gsteps,
+                                                        const int64_t *__restrict__ j0s,
+                                                        const double *__restrict__ u0,
+                                                        double *__restrict__ uF) {
+    using T = Tableau<ORDER>;
+    constexpr int S = T::S;
+    extern __shared__ __attribute__((aligned(16))) double smem[];   // [2][d]
+    const int slice = blockIdx.x;
+    const int tid = threadIdx.x, BT = blockDim.x;
+    const int d = fa.d;
+    const int half = d / 2;   // FHN-PDE: u1 | u2
+
+    double u[EPT], k[S][EPT], mn[EPT], w[EPT], sc[EPT];
+    int e_[EPT];
+    Nbr5 nb[(SYS == NNGP_SYS_FHN_PDE) ? EPT : 1];
+#pragma unroll
+    for (int r = 0; r < EPT; r++) {
+        const int e = tid + r * BT;
+        e_[r] = e;
+        const bool ok = e < d;
+        u[r] = ok ? u0[(size_t)slice * d + e] : 0.0;
+        if (fa.normalized && ok) {
+            mn[r] = fa.norm[e];
+            w[r] = fa.norm[d + e];
+            sc[r] = fa.norm[2 * d + e];
+        } else {
+            mn[r] = 0.0; w[r] = 1.0; sc[r] = 1.0;
+        }
+        if constexpr (SYS == NNGP_SYS_FHN_PDE) nb[r] = fhn_neighbours(fa.nx, ok ? (e % half) : 0);
+    }
+    const double T0 = t0[slice], T1 = t1[slice];
+    const double dt = (T1 - T0) / (double)(LINSPACE ? gsteps : steps);
+    const int64_t j0 = j0s ? j0s[slice] : 0;
+    int buf = 0;
+    for (int64_t n = 0; n < steps; n++) {
+        const double h = step_size(LINSPACE, n, j0, gsteps, T0, T1, dt);
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+            double *V = smem + buf * d;
+#pragma unroll
+            for (int r = 0; r < EPT; r++) {
+                if (e_[r] < d) {
+                    double x = u[r];
+                    if (s > 0) {
+                        double t = 0.0;
+#pragma unroll
+                        for (int j = 0; j < s; j++)
+                            if (T::A[s][j] != 0.0) t = t + T::A[s][j] * k[j][r];
+                        x = u[r] + t;
+                    }
+                    V[e_[r]] = fa.normalized ? ((x + 1) / 2) * w[r] + mn[r] : x;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < EPT; r++) {
+                const int e = e_[r];
+                double f = 0.0;
+                if (e < d) {
+                    if constexpr (SYS == NNGP_SYS_BURGERS) {
+                        f = burgers_elem(V, e, d, fa);
+                    } else {   // FHN_PDE, systems.py:365-366
+                        if (e < half) {
+                            const double lu = fhn_lap(V, nb[r], fa.a_off, fa.a_diag);
+                            const double u1 = V[e], u1c = u1 * (u1 * u1);
+                            f = (((lu + u1) - u1c) - V[half + e]) + -5E-3 * 1.0;
+                        } else {
+                            const double lv = fhn_lap(V + half, nb[r], fa.b_off, fa.b_diag);
+                            f = (1 / 0.1) * ((lv + V[e - half]) - V[e]);
+                        }
+                    }
+                    if (fa.normalized) f = f * sc[r];
+                }
+                k[s][r] = h * f;
+            }
+            buf ^= 1;
+        }
+#pragma unroll
+        for (int r = 0; r < EPT; r++) {
+            double acc = 0.0;
+            bool first = true;
+#pragma unroll
+            for (int s = 0; s < S; s++) {
+                if (T::B[s] == 0.0) continue;
+                const double v = T::B[s] * k[s][r];
+                acc = first ? v : acc + v;
+                first = false;
+            }
+            u[r] = u[r] + acc;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < EPT; r++)
+        if (e_[r] < d) uF[(size_t)slice * d + e_[r]] = u[r];
+}
+
+// ---------------------------------------------------------------------------------------------
+// single RHS evaluations (ODE.get_vector_field()(t, u)) and the elementwise Parareal update
+// ---------------------------------------------------------------------------------------------
+template <int SYS>
+__global__ void __launch_bounds__(64) rhs_lane_kernel(LaneArgs args, int n, const double *__restrict__ u,
+                                                      double *__restrict__ out) {
+    constexpr int D = LaneSys<SYS>::D;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (args.normalized)
+        for (int c = 0; c < D; c++) {
+            args.mn[c] = args.norm[c];
+            args.w[c] = args.norm[D + c];
+            args.sc[c] = args.norm[2 * D + c];
+        }
+    double x[D], o[D];
+    for (int c = 0; c < D; c++) x[c] = u[(size_t)i * D + c];
+    lane_rhs<SYS>(x, o, args);
+    for (int c = 0; c < D; c++) out[(size_t)i * D + c] = o[c];
+}
+
+template <int SYS>
+__global__ void __launch_bounds__(256) rhs_field_kernel(FieldArgs fa, const double *__restrict__ u,
+                                                        double *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) double V[];
+    const int d = fa.d, half = d / 2, s = blockIdx.x;
+    for (int e = threadIdx.x; e < d; e += blockDim.x) {
+        const double x = u[(size_t)s * d + e];
+        V[e] = fa.normalized ? ((x + 1) / 2) * fa.norm[d + e] + fa.norm[e] : x;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < d; e += blockDim.x) {
+        double f;
+        if constexpr (SYS == NNGP_SYS_BURGERS) {
+            f = burgers_elem(V, e, d, fa);
+        } else if (e < half) {
+            const Nbr5 nb = fhn_neighbours(fa.nx, e);
+            const double u1 = V[e];
+            f = (((fhn_lap(V, nb, fa.a_off, fa.a_diag) + u1) - u1 * (u1 * u1)) - V[half + e]) + -5E-3 * 1.0;
+        } else {
+            const Nbr5 nb = fhn_neighbours(fa.nx, e - half);
+            f = (1 / 0.1) * ((fhn_lap(V + half, nb, fa.b_off, fa.b_diag) + V[e - half]) - V[e]);
+        }
+        out[(size_t)s * d + e] = fa.normalized ? f * fa.norm[2 * d + e] : f;
+    }
+}
+
+__global__ void __launch_bounds__(256) update_kernel(int64_t n, const double *__restrict__ a,
+                                                     const double *__restrict__ b,
+                                                     const double *__restrict__ c,
+                                                     double *__restrict__ out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const double p = a[i] - b[i];
+        out[i] = c ? p + c[i] : p;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host dispatch
+// ---------------------------------------------------------------------------------------------
+template <int SYS, int ORDER, bool LIN>
+static int launch_lane(const nngp_system *sys, int n, const double *t0, const double *t1,
+                       int64_t steps, int64_t gsteps, const int64_t *j0, const double *u0, double *uF,
+                       hipStream_t st) {
+    LaneArgs a{};
+    constexpr int D = LaneSys<SYS>::D;
+    NNGP_REQUIRE(sys->d == D, "system kind %d has d=%d, got d=%d", SYS, D, sys->d);
+    a.normalized = sys->normalized;
+    for (int c = 0; c < 4; c++) a.param[c] = sys->param[c];
+    a.norm = sys->norm;
+    NNGP_REQUIRE(!sys->normalized || sys->norm != nullptr, "normalized system needs norm[3d]");
+    const int bs = 64;
+    hipLaunchKernelGGL((rk_lane_kernel<SYS, ORDER, LIN>), dim3((n + bs - 1) / bs), dim3(bs), 0, st,
+                       a, n, t0, t1, steps, gsteps, j0, u0, uF);
+    NNGP_LAUNCH_CHECK();
+    return NNGP_OK;
+}
+
+template <int SYS, int ORDER, bool LIN, int EPT>
+static int launch_field_ept(const FieldArgs &fa, int bt, int n, const double *t0,
+                            const double *t1, int64_t steps, int64_t gsteps, const int64_t *j0,
+                            const double *u0, double *uF, hipStream_t st) {
+    const size_t lds = sizeof(double) * 2 * (size_t)fa.d;
+    hipLaunchKernelGGL((rk_field_kernel<SYS, ORDER, LIN, EPT>), dim3(n), dim3(bt), lds, st, fa, n,
+                       t0, t1, steps, gsteps, j0, u0, uF);
+    NNGP_LAUNCH_CHECK();
+    return NNGP_OK;
+}
+
+// threads per slice: env NNGP_RK_THREADS overrides (tuning), else the fewest whole waves that
+// keep EPT <= 4 (d=128 -> 64 threads x 2, d=800 -> 256 threads x 4)
+static int pick_threads(int d) {
+    const char *env = getenv("NNGP_RK_THREADS");
+    if (env) {
+        int v = atoi(env);
+        if (v >= 64 && v <= 256 && v % 64 == 0) return v;
+    }
+    int bt = 64;
+    while (bt < 256 && (d + bt - 1) / bt > 4) bt += 64;
+    return bt;
+}
+
+static int field_args(const nngp_system *sys, FieldArgs &fa) {
+    fa = FieldArgs{};
+    fa.d = sys->d;
+    fa.nx = sys->nx;
+    fa.normalized = sys->normalized;
+    fa.norm = sys->norm;
+    NNGP_REQUIRE(!sys->normalized || sys->norm, "normalized system needs norm[3d]");
+    if (sys->kind == NNGP_SYS_BURGERS) {
+        NNGP_REQUIRE(sys->nx == sys->d && sys->d >= 3, "Burgers needs nx == d >= 3");
+        const double dx = (1.0 - (-1.0)) / (sys->d - 1);
+        const double nu = sys->param[0];
+        fa.c_off = nu / (dx * dx);   // (nu/dx**2)*Txx
+        fa.c_diag = fa.c_off * -2.0;
+        fa.c_grad = 1 / (2 * dx);    // (1/(2*dx))*Tx
+    } else {
+        NNGP_REQUIRE(sys->nx >= 3 && sys->d == 2 * sys->nx * sys->nx, "FHN_PDE needs d = 2 nx^2, nx >= 3");
+        const double dx = (1.0 - (-1.0)) / (sys->nx - 1);
+        const double c1 = 1 / (dx * dx);
+        const double ldiag = c1 * -2.0 + c1 * -2.0;   // (DXX + DYY) diagonal
+        fa.a_off = 2.8E-4 * c1;
+        fa.a_diag = 2.8E-4 * ldiag;
+        fa.b_off = 5E-3 * c1;
+        fa.b_diag = 5E-3 * ldiag;
+    }
+    NNGP_REQUIRE(sizeof(double) * 2 * (size_t)sys->d <= 160 * 1024, "LDS image too large");
+    return NNGP_OK;
+}
+
+template <int SYS, int ORDER, bool LIN>
+static int launch_field(const nngp_system *sys, int n, const double *t0, const double *t1,
+                        int64_t steps, int64_t gsteps, const int64_t *j0, const double *u0, double *uF,
+                        hipStream_t st) {
+    FieldArgs fa;
+    int rc = field_args(sys, fa);
+    if (rc) return rc;
+    const int bt = pick_threads(sys->d);
+    const int ept = (sys->d + bt - 1) / bt;
+    NNGP_REQUIRE(ept <= 8, "d=%d too large for the field kernel (max 2048)", sys->d);
+    if (ept <= 1) return launch_field_ept<SYS, ORDER, LIN, 1>(fa, bt, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    if (ept <= 2) return launch_field_ept<SYS, ORDER, LIN, 2>(fa, bt, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    if (ept <= 4) return launch_field_ept<SYS, ORDER, LIN, 4>(fa, bt, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    return launch_field_ept<SYS, ORDER, LIN, 8>(fa, bt, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+}
+
+template <int ORDER, bool LIN>
+static int dispatch_sys(const nngp_system *s, int n, const double *t0, const double *t1,
+                        int64_t steps, int64_t gsteps, const int64_t *j0, const double *u0,
+                        double *uF, hipStream_t st) {
+    switch (s->kind) {
+    case NNGP_SYS_LORENZ: return launch_lane<NNGP_SYS_LORENZ, ORDER, LIN>(s, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    case NNGP_SYS_HOPF: return launch_lane<NNGP_SYS_HOPF, ORDER, LIN>(s, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    case NNGP_SYS_THOMAS_LABYRINTH:
+        return launch_lane<NNGP_SYS_THOMAS_LABYRINTH, ORDER, LIN>(s, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    case NNGP_SYS_FHN_ODE: return launch_lane<NNGP_SYS_FHN_ODE, ORDER, LIN>(s, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    case NNGP_SYS_ROSSLER: return launch_lane<NNGP_SYS_ROSSLER, ORDER, LIN>(s, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    case NNGP_SYS_BRUSSELATOR:
+        return launch_lane<NNGP_SYS_BRUSSELATOR, ORDER, LIN>(s, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    case NNGP_SYS_DBL_PEND: return launch_lane<NNGP_SYS_DBL_PEND, ORDER, LIN>(s, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    case NNGP_SYS_BURGERS: return launch_field<NNGP_SYS_BURGERS, ORDER, LIN>(s, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    case NNGP_SYS_FHN_PDE: return launch_field<NNGP_SYS_FHN_PDE, ORDER, LIN>(s, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    default: set_error("unknown system kind %d", s->kind); return NNGP_E_ARG;
+    }
+}
+
+template <bool LIN>
+static int dispatch_tab(const nngp_system *s, int tab, int n, const double *t0, const double *t1,
+                        int64_t steps, int64_t gsteps, const int64_t *j0, const double *u0,
+                        double *uF, hipStream_t st) {
+    switch (tab) {
+    case NNGP_RK1: return dispatch_sys<1, LIN>(s, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    case NNGP_RK2: return dispatch_sys<2, LIN>(s, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    case NNGP_RK4: return dispatch_sys<4, LIN>(s, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    case NNGP_RK8: return dispatch_sys<8, LIN>(s, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    default: set_error("unknown tableau %d (RK1/2/4/8)", tab); return NNGP_E_ARG;
+    }
+}
+
+template <int SYS>
+static int launch_rhs_lane(const nngp_system *sys, int n, const double *u, double *out, hipStream_t st) {
+    LaneArgs a{};
+    NNGP_REQUIRE(sys->d == LaneSys<SYS>::D, "system kind %d has d=%d, got d=%d", SYS, LaneSys<SYS>::D, sys->d);
+    NNGP_REQUIRE(!sys->normalized || sys->norm != nullptr, "normalized system needs norm[3d]");
+    a.normalized = sys->normalized;
+    a.norm = sys->norm;
+    for (int c = 0; c < 4; c++) a.param[c] = sys->param[c];
+    hipLaunchKernelGGL(rhs_lane_kernel<SYS>, dim3((n + 63) / 64), dim3(64), 0, st, a, n, u, out);
+    NNGP_LAUNCH_CHECK();
+    return NNGP_OK;
+}
+
+template <int SYS>
+static int launch_rhs_field(const nngp_system *sys, int n, const double *u, double *out, hipStream_t st) {
+    FieldArgs fa;
+    int rc = field_args(sys, fa);
+    if (rc) return rc;
+    hipLaunchKernelGGL(rhs_field_kernel<SYS>, dim3(n), dim3(256), sizeof(double) * sys->d, st, fa, u, out);
+    NNGP_LAUNCH_CHECK();
+    return NNGP_OK;
+}
+
+}  // namespace nngp
+
+extern "C" int nngp_rhs_batch(const nngp_system *sys, int n, const double *u, double *out, void *stream) {
+    using namespace nngp;
+    NNGP_REQUIRE(sys != nullptr && n >= 0, "bad sys / n");
+    if (n == 0) return NNGP_OK;
+    NNGP_REQUIRE(u && out, "null array argument");
+    hipStream_t st = (hipStream_t)stream;
+    switch (sys->kind) {
+    case NNGP_SYS_LORENZ: return launch_rhs_lane<NNGP_SYS_LORENZ>(sys, n, u, out, st);
+    case NNGP_SYS_HOPF: return launch_rhs_lane<NNGP_SYS_HOPF>(sys, n, u, out, st);
+    case NNGP_SYS_THOMAS_LABYRINTH: return launch_rhs_lane<NNGP_SYS_THOMAS_LABYRINTH>(sys, n, u, out, st);
+    case NNGP_SYS_FHN_ODE: return launch_rhs_lane<NNGP_SYS_FHN_ODE>(sys, n, u, out, st);
+    case NNGP_SYS_ROSSLER: return launch_rhs_lane<NNGP_SYS_ROSSLER>(sys, n, u, out, st);
+    case NNGP_SYS_BRUSSELATOR: return launch_rhs_lane<NNGP_SYS_BRUSSELATOR>(sys, n, u, out, st);
+    case NNGP_SYS_DBL_PEND: return launch_rhs_lane<NNGP_SYS_DBL_PEND>(sys, n, u, out, st);
+    case NNGP_SYS_BURGERS: return launch_rhs_field<NNGP_SYS_BURGERS>(sys, n, u, out, st);
+    case NNGP_SYS_FHN_PDE: return launch_rhs_field<NNGP_SYS_FHN_PDE>(sys, n, u, out, st);
+    default: set_error("unknown system kind %d", sys->kind); return NNGP_E_ARG;
+    }
+}
+
+extern "C" int nngp_parareal_update(int64_t n, const double *a, const double *b, const double *c,
+                                    double *out, void *stream) {
+    using namespace nngp;
+    NNGP_REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return NNGP_OK;
+    NNGP_REQUIRE(a && b && out, "null array argument");
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(update_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n, a, b, c, out);
+    NNGP_LAUNCH_CHECK();
+    return NNGP_OK;
+}
+
+extern "C" int nngp_rk_batch(const nngp_system *sys, int tableau, int step_mode, int n_slices,
+                             const double *t0, const double *t1, int64_t steps, const double *u0,
+                             double *uF, void *stream) {
+    using namespace nngp;
+    NNGP_REQUIRE(sys != nullptr, "sys is NULL");
+    NNGP_REQUIRE(n_slices >= 0, "n_slices < 0");
+    NNGP_REQUIRE(steps >= 1, "steps must be >= 1 (got %lld)", (long long)steps);
+    if (n_slices == 0) return NNGP_OK;
+    NNGP_REQUIRE(t0 && t1 && u0 && uF, "null array argument");
+    hipStream_t st = (hipStream_t)stream;
+    if (step_mode == NNGP_STEP_FIXED)
+        return dispatch_tab<false>(sys, tableau, n_slices, t0, t1, steps, steps, nullptr, u0, uF, st);
+    if (step_mode == NNGP_STEP_LINSPACE)
+        return dispatch_tab<true>(sys, tableau, n_slices, t0, t1, steps, steps, nullptr, u0, uF, st);
+    set_error("unknown step_mode %d", step_mode);
+    return NNGP_E_ARG;
+}
+
+extern "C" int nngp_rk_batch_grid(const nngp_system *sys, int tableau, int n_slices,
+                                  const double *g0, const double *g1, int64_t gsteps,
+                                  const int64_t *j0, int64_t steps, const double *u0, double *uF,
+                                  void *stream) {
+    using namespace nngp;
+    NNGP_REQUIRE(sys != nullptr, "sys is NULL");
+    NNGP_REQUIRE(n_slices >= 0 && steps >= 1 && gsteps >= 1, "bad n_slices / steps / gsteps");
+    if (n_slices == 0) return NNGP_OK;
+    NNGP_REQUIRE(g0 && g1 && j0 && u0 && uF, "null array argument");
+    return dispatch_tab<true>(sys, tableau, n_slices, g0, g1, steps, gsteps, j0, u0, uF,
+                              (hipStream_t)stream);
+}

@@ -1,0 +1,249 @@
+"""Correction models -- the reference's ModelAbstr / BareParareal / NNGP_p plugin surface
+(models.py:19-270) with the nearest-neighbour GP running on the GPU.
+
+NNGP_p keeps the reference's constructor arguments (n, N, worker_pool, theta, fatol, xatol, nn,
+seed, n_restarts, ...), its RNG (np.random.default_rng(seed), models.py:114) and the exact order
+of its draws: per prediction, rng.integers(-8, 0, 2) once for every (coordinate, jitter,
+restart) in itertools.product order (models.py:186-192).  A single vectorised
+rng.integers(-8, 0, (count, 2)) yields the same stream (the range is a power of two, so
+numpy's Lemire sampler never rejects; pinned by tests/test_host.py against tests/golden/rng.npz).
+
+Compute paths (all HIP, no CPU fallback):
+  predict(...)         reference signature, host arrays in/out -> nngp_predict (fused kernels)
+  predict_device(...)  device tensors, used by the Parareal driver's sequential loop
+  get_preds(...)       reference signature on pre-selected (xm, ym) -> nngp_nm_fit_batch +
+                       first-argmin + nngp_gp_mean (the unfused path of the same kernels)
+"""
+import copy
+import ctypes
+import time
+from itertools import product
+
+import numpy as np
+
+from . import _lib
+
+JITTERS = np.arange(-20, -11, dtype=float)   # models.py:186
+
+
+class ModelAbstr():
+
+    def __init__(self, **kwargs):
+        self.train_time = 0
+        self.pred_time = 0
+        N = kwargs['N']
+        self.pred_times = np.zeros(N)
+        self.time_k = 0
+
+    def fit_timed(self, x, y, *args, **kwargs):
+        self.time_k = kwargs['k']
+        s_time = time.time()
+        ret = self.fit(x, y, *args, **kwargs)
+        elap_time = time.time() - s_time
+        self.train_time += elap_time
+        self.pred_times[self.time_k] += elap_time
+        return ret
+
+    def predict_timed(self, new_x, *args, **kwargs):
+        s_time = time.time()
+        ret = self.predict(new_x, *args, **kwargs)
+        elap_time = time.time() - s_time
+        self.pred_time += elap_time
+        self.pred_times[self.time_k] += elap_time
+        return ret
+
+    def add_pred_time(self, seconds):
+        """Device-measured prediction time (the Parareal driver times whole sweeps with events)."""
+        self.pred_time += seconds
+        self.pred_times[self.time_k] += seconds
+
+    def get_times(self):
+        return {'mdl_train_t': self.train_time, 'mdl_pred_t': self.pred_time,
+                'mdl_tot_t': self.train_time + self.pred_time, 'by_iter': self.pred_times[:self.time_k + 1]}
+
+    def fit(self, x, y, *args, **kwargs):
+        self.x, self.y = x, y
+        raise Exception('Not implemented')
+
+    def predict(self, new_x, prev_F, prev_G):
+        raise Exception('Not implemented')
+
+    def store(self):
+        if hasattr(self, 'pool'):
+            pool = self.pool
+            self.pool = None
+            new = copy.deepcopy(self)
+            self.pool = pool
+        else:
+            new = copy.deepcopy(self)
+        return new
+
+
+class BareParareal(ModelAbstr):
+    """Classic Parareal correction F - G (models.py:74-83)."""
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        self.name = 'Parareal'
+
+    def fit(self, *args, **kwargs):
+        pass
+
+    def predict(self, new_x, prev_F, prev_G, *args, **kwargs):
+        return prev_F - prev_G
+
+
+class NNGP_p(ModelAbstr):
+    """Nearest-neighbour GP correction (models.py:98-270) on the GPU."""
+
+    def __init__(self, n, N, worker_pool=None, theta=None, fatol=None, xatol=None, **kwargs):
+        super().__init__(N=N, **kwargs)
+        if theta is None:
+            theta = [1, 1]
+        self.theta = np.array(theta)
+        self.name = 'NNGP'
+        self.fatol = 1e-1 if fatol is None else fatol
+        self.xatol = 1e-1 if xatol is None else xatol
+        self.n = n
+        self.n_restarts = kwargs.get('n_restarts', 1)
+        self.nn = kwargs.get('nn', 'adaptive')
+        self.seed = kwargs.get('seed', 45)
+        self.rng = np.random.default_rng(self.seed)
+        np.random.seed(self.seed)
+        self.pool = worker_pool
+        self.maxfev = 200 * len(self.theta)   # scipy default maxiter = maxfev = 200*N
+        self.tot_train_t = 0
+        self.train_count = 0
+        self.k = 0
+        self._dev_xy = None
+
+    # ------------------------------------------------------------------------------ helpers
+    @property
+    def n_fits(self):
+        return self.n * len(JITTERS) * self.n_restarts
+
+    def n_neighbours(self):
+        return max(10, self.k + 2) if self.nn == 'adaptive' else int(self.nn)   # models.py:172-175
+
+    def draw_thetas(self, n_predictions):
+        """Initial thetas for `n_predictions` consecutive predictions (models.py:192)."""
+        return self.rng.integers(-8, 0, (n_predictions * self.n_fits, len(self.theta))).astype(np.float64)
+
+    def get_times(self):
+        out = super().get_times()
+        out.update({'serial_train_time': self.tot_train_t, 'calc_detail_avg': None, 'overhead': None,
+                    'avg_serial_train_time': self.tot_train_t / max(self.train_count, 1)})
+        return out
+
+    def fit(self, x, y, k, *args, **kwargs):
+        self.k = k
+        self.x, self.y = x, y
+        self._dev_xy = None
+
+    # ---------------------------------------------------------------------------- device path
+    def predict_device(self, X, Y, rows, new_x, theta0, out=None, bias=None, preds=None,
+                       fits_out=None, stream=None):
+        """One correction on device tensors.  X/Y: [>=rows][n] training set, new_x: [n],
+        theta0: [n_fits][2] (this prediction's draws).  Writes preds (and out = preds + bias)."""
+        import torch
+        m = min(self.n_neighbours(), int(rows))   # argsort(...)[:nn] on fewer rows keeps them all
+        if preds is None:
+            preds = torch.empty(self.n, dtype=torch.float64, device=X.device)
+        jit, jp = _lib.host_doubles(JITTERS)
+        st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        _lib.check(_lib.lib().nngp_predict(
+            X.data_ptr(), Y.data_ptr(), int(rows), self.n, new_x.data_ptr(), m, len(jit), jp,
+            self.n_restarts, theta0.data_ptr(), float(self.fatol), float(self.xatol), self.maxfev,
+            preds.data_ptr(), bias.data_ptr() if bias is not None else None,
+            out.data_ptr() if out is not None else None,
+            fits_out.data_ptr() if fits_out is not None else None, st))
+        self.train_count += self.n_fits
+        return preds
+
+    # ------------------------------------------------------------------------- reference API
+    def predict(self, new_x, prev_F=None, prev_G=None, *args, **kwargs):
+        """models.py:171-183 (host arrays in/out; kNN + fits + argmin + mean on the GPU)."""
+        torch = _lib.require_gpu()
+        if self._dev_xy is None:
+            self._dev_xy = (torch.tensor(np.ascontiguousarray(self.x, dtype=np.float64), device='cuda'),
+                            torch.tensor(np.ascontiguousarray(self.y, dtype=np.float64), device='cuda'))
+        X, Y = self._dev_xy
+        q = torch.tensor(np.asarray(new_x, dtype=np.float64).reshape(-1), device='cuda')
+        th0 = torch.tensor(self.draw_thetas(1), device='cuda')
+        preds = self.predict_device(X, Y, X.shape[0], q, th0)
+        return preds.cpu().numpy()
+
+    def get_preds(self, xm, ym, n, new_x, intrvl_i):
+        """models.py:185-226 on already-selected neighbours: all fits, first argmin, mean."""
+        torch = _lib.require_gpu()
+        m = xm.shape[0]
+        ins = list(product(range(n), range(len(JITTERS)), range(self.n_restarts)))
+        th0 = self.draw_thetas(1)
+        res = self.fit_batch(xm, ym, [i[0] for i in ins], [i[1] for i in ins], th0)
+        preds = np.empty(n)
+        best_th = np.empty((n, 2))
+        best_j = np.empty(n, dtype=np.int32)
+        per = len(JITTERS) * self.n_restarts
+        for j in range(n):
+            fv = res['fval'][j * per:(j + 1) * per]
+            b = int(np.argmin(fv))                  # first minimum == models.py:212-215
+            best_th[j] = res['theta'][j * per + b]
+            best_j[j] = ins[j * per + b][1]
+        preds[:] = self.gp_mean(xm, ym, new_x, best_th, best_j)
+        return preds
+
+    def fit_batch(self, xm, ym, coords, jitter_idx, theta0):
+        """pool.map(_get_opt_par, ...) as one launch (nngp_nm_fit_batch)."""
+        torch = _lib.require_gpu()
+        xm_t = torch.tensor(np.ascontiguousarray(xm, dtype=np.float64), device='cuda')
+        ym_t = torch.tensor(np.ascontiguousarray(ym, dtype=np.float64), device='cuda')
+        nf = len(coords)
+        c_t = torch.tensor(np.asarray(coords, dtype=np.int32), device='cuda')
+        j_t = torch.tensor(np.asarray(jitter_idx, dtype=np.int32), device='cuda')
+        th_t = torch.tensor(np.ascontiguousarray(theta0, dtype=np.float64), device='cuda')
+        th_o = torch.empty((nf, 2), dtype=torch.float64, device='cuda')
+        fv_o = torch.empty(nf, dtype=torch.float64, device='cuda')
+        ne_o = torch.empty(nf, dtype=torch.int32, device='cuda')
+        jit, jp = _lib.host_doubles(JITTERS)
+        st = torch.cuda.current_stream().cuda_stream
+        _lib.check(_lib.lib().nngp_nm_fit_batch(
+            xm.shape[0], xm.shape[1], xm_t.data_ptr(), ym_t.data_ptr(), nf, c_t.data_ptr(), j_t.data_ptr(),
+            len(jit), jp, th_t.data_ptr(), float(self.fatol), float(self.xatol), self.maxfev,
+            th_o.data_ptr(), fv_o.data_ptr(), ne_o.data_ptr(), st))
+        self.train_count += nf
+        return {'theta': th_o.cpu().numpy(), 'fval': fv_o.cpu().numpy(), 'nfev': ne_o.cpu().numpy()}
+
+    def gp_mean(self, xm, ym, new_x, theta, jitter_idx):
+        torch = _lib.require_gpu()
+        n = ym.shape[1]
+        xm_t = torch.tensor(np.ascontiguousarray(xm, dtype=np.float64), device='cuda')
+        ym_t = torch.tensor(np.ascontiguousarray(ym, dtype=np.float64), device='cuda')
+        q = torch.tensor(np.asarray(new_x, dtype=np.float64).reshape(-1), device='cuda')
+        th = torch.tensor(np.ascontiguousarray(theta, dtype=np.float64), device='cuda')
+        ji = torch.tensor(np.asarray(jitter_idx, dtype=np.int32), device='cuda')
+        out = torch.empty(n, dtype=torch.float64, device='cuda')
+        jit, jp = _lib.host_doubles(JITTERS)
+        _lib.check(_lib.lib().nngp_gp_mean(xm.shape[0], n, xm_t.data_ptr(), ym_t.data_ptr(), q.data_ptr(),
+                                            th.data_ptr(), ji.data_ptr(), len(jit), jp, out.data_ptr(),
+                                            torch.cuda.current_stream().cuda_stream))
+        return out.cpu().numpy()
+
+    @staticmethod
+    def _get_opt_par(static_ins, ins, rnd):
+        """models.py:228-237: one fit -> (*theta, fval, jitter, j, elapsed)."""
+        st_ = time.time()
+        xm, ym, fatol, xatol = static_ins
+        j, jitter, _ = ins
+        tmp = NNGP_p(n=ym.shape[1], N=1, fatol=fatol, xatol=xatol)
+        jidx = int(np.where(JITTERS == jitter)[0][0])
+        r = tmp.fit_batch(xm, ym, [j], [jidx], np.asarray(rnd, dtype=float).reshape(1, 2))
+        return (*r['theta'][0], r['fval'][0], jitter, j, time.time() - st_)
+
+    def store(self):
+        new = super().store()
+        new.pool = None
+        new._dev_xy = None
+        return new
+
+    def restore_attrs(self, pool):
+        self.pool = pool

@@ -1,0 +1,289 @@
+"""Parareal driver -- the reference's Parareal(ode, solver, tspan, N, epsilon).run(model=...,
+pool=..., parall=..., nn=..., seed=...) surface (parareal.py:26-471) with a device-resident loop.
+
+Per iteration k (parareal.py:301-439):
+  1. F over the unconverged slices [I, N): ONE nngp_rk_batch launch (replaces
+     pool.map(solver.run_F_timed, ...) at :310-315).  With torch.distributed initialised and
+     world_size > 1 the slices are split into contiguous blocks, one per rank/GPU, followed by a
+     single all-gather of the fine end states (RCCL over xGMI) -- the only collective.
+  2. training-set growth (:331-339) appended on the device (no host round trip).
+  3. the SEQUENTIAL correction sweep i = I..N-1 (:359-382): G (one-slice nngp_rk_batch),
+     model prediction (nngp_predict, or the classic F-G update), u[i+1] = preds + uG[i+1] -- all
+     queued on one HIP stream without host synchronisation; the sweep is replicated on every rank
+     (same inputs, same RNG draws), so ranks stay bit-identical without a broadcast.
+  4. one device->host copy of the new column, then the error / convergence scan (:396-416) on
+     the host exactly as the reference does.
+The returned dict has the reference's keys ('t', 'u', 'err', 'x', 'D', 'k', 'data_x', 'data_D',
+'timings', 'debug_dict', 'converged', 'conv_int').
+"""
+import ctypes
+import time
+import warnings
+
+import numpy as np
+
+from . import _lib
+from .models import BareParareal, NNGP_p
+from .solver import SolverAbstr
+from .systems import ODE
+
+
+class MyPool():
+    """Serial executor of the reference (parareal.py:16-24)."""
+
+    @staticmethod
+    def map(*args, chunksize=None, **kwargs):
+        return map(*args, **kwargs)
+
+    @staticmethod
+    def shutdown(*args, **kwargs):
+        pass
+
+
+class GpuPool(MyPool):
+    """Executor stand-in: the work the reference fans out through pool.map (fine solves, GP fits)
+    is batched into single GPU launches by the driver and models, so the pool itself only has to
+    provide the reference's map/shutdown surface."""
+
+
+class _Events:
+    def __init__(self, torch):
+        self.torch = torch
+        self.pairs = []
+
+    def start(self):
+        e = self.torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def stop(self, start, bucket):
+        e = self.torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.pairs.append((start, e, bucket))
+
+    def collect(self):
+        out = {}
+        for a, b, k in self.pairs:
+            out[k] = out.get(k, 0.0) + a.elapsed_time(b) / 1e3
+        self.pairs = []
+        return out
+
+
+class Parareal():
+
+    def __init__(self, ode, solver, tspan, N, epsilon=5e-7, verbose='v', process_group=None, **kwargs):
+        if not isinstance(ode, ODE):
+            raise Exception('ode must be an instance of the ODE class, see systems.py file.')
+        if not isinstance(solver, SolverAbstr):
+            raise Exception('solver must be an instance of the SolverAbstr class, see solver.py file.')
+        self.tspan = tspan
+        self.N = N
+        self.epsilon = epsilon
+        self.runs = dict()
+        self.fine = None
+        self.ode_name = ode.name
+        self.n = ode.get_dim()
+        self.ode = ode
+        self.solver = solver
+        self.f = ode.get_vector_field()
+        self.u0 = ode.get_init_cond()
+        self.verbose = verbose
+        self.process_group = process_group
+
+    def _get_pool(self, *args, **kwargs):
+        pool = kwargs.get('pool', None)
+        if pool is None or isinstance(pool, int):
+            pool = GpuPool()   # no worker processes: the fan-outs are GPU launches
+        return pool
+
+    def run(self, *args, **kwargs):
+        pool = self._get_pool(*args, **kwargs)
+        kwargs['pool'] = pool
+        try:
+            out = self._run(*args, **kwargs)
+        except Exception:
+            pool.shutdown()
+            raise
+        pool.shutdown()
+        return out
+
+    def _run(self, model='parareal', cstm_mdl_name=None, add_model=False, **kwargs):
+        if model.lower() == 'parareal':
+            mdl = BareParareal(N=self.N, **kwargs)
+        elif model.lower() == 'nngp':
+            mdl = NNGP_p(n=self.n, N=self.N, worker_pool=kwargs['pool'], **kwargs)
+        elif model.lower() in ('gpjax', 'elm'):
+            raise NotImplementedError(f'model {model!r} is outside the nnGP hot path (SURVEY.md §8f)')
+        else:
+            raise Exception('Not implemented')
+        s_time = time.time()
+        out = self._parareal(mdl, **kwargs)
+        elap_time = time.time() - s_time
+        out['timings']['runtime'] = elap_time
+        if self.verbose == 'v':
+            print(f'Elapsed Parareal time: {elap_time:0.2f}s')
+        if add_model:
+            out['mdl'] = mdl.store()
+        if cstm_mdl_name is None:
+            cstm_mdl_name = mdl.name
+        self.runs[cstm_mdl_name] = out
+        return out
+
+    # ------------------------------------------------------------------------------ F sweep
+    def _fine_sweep(self, torch, t_dev, Uk, UF, I, N, n):
+        """uF[I+1:N+1] = F(u[I:N]) -- sharded over ranks when a process group is active."""
+        pg = self.process_group
+        world = 1
+        if pg is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
+            world = torch.distributed.get_world_size(pg)
+        if world == 1:
+            self.solver.run_F_batch(t_dev[I:N], t_dev[I + 1:N + 1], Uk[I:N], out=UF[I + 1:N + 1])
+            return
+        rank = torch.distributed.get_rank(pg)
+        n_c = N - I
+        chunk = (n_c + world - 1) // world
+        lo = I + min(rank * chunk, n_c)
+        hi = I + min((rank + 1) * chunk, n_c)
+        send = torch.zeros((chunk, n), dtype=torch.float64, device=Uk.device)
+        if hi > lo:
+            self.solver.run_F_batch(t_dev[lo:hi], t_dev[lo + 1:hi + 1], Uk[lo:hi].contiguous(),
+                                    out=send[:hi - lo])
+        gathered = torch.empty((world * chunk, n), dtype=torch.float64, device=Uk.device)
+        torch.distributed.all_gather_into_tensor(gathered, send, group=pg)
+        UF[I + 1:N + 1] = gathered[:n_c]
+
+    # --------------------------------------------------------------------------- main loop
+    def _parareal(self, model, debug=False, early_stop=None, parall='Serial', store_int=False,
+                  **kwargs):
+        torch = _lib.require_gpu()
+        if debug:
+            warnings.warn('debug mode (per-slice fine re-solves) is not supported; ignored')
+        if store_int:
+            warnings.warn('store_int checkpoints are not implemented yet (SURVEY.md §8f row 4); ignored')
+        tspan, N, epsilon, n = self.tspan, self.N, self.epsilon, self.n
+        solver = self.solver
+        verbose = kwargs.get('verbose', self.verbose)
+        dev = torch.device('cuda', torch.cuda.current_device())
+        f64 = dict(dtype=torch.float64, device=dev)
+        lib = _lib.lib()
+        stream = torch.cuda.current_stream().cuda_stream
+        ev = _Events(torch)
+        is_nngp = isinstance(model, NNGP_p)
+
+        t = np.linspace(tspan[0], tspan[1], num=N + 1)
+        t_dev = torch.tensor(t, **f64)
+        I = 0
+        conv_int = []
+        u = np.full((N + 1, n, N + 1), np.nan)
+        err = np.full((N + 1, N), np.nan)
+        x = np.zeros((0, n))
+        D = np.zeros((0, n))
+        data_x = np.full((N, n, N), np.nan)
+        data_D = np.full((N, n, N), np.nan)
+        G_time = F_time = F_time_serial = 0.0
+
+        u0 = torch.tensor(self.u0, **f64)
+        Uk = torch.empty((N + 1, n), **f64)
+        UGk = torch.empty((N + 1, n), **f64)
+        UF = torch.empty((N + 1, n), **f64)
+        UGk[0] = u0
+        UF[0] = u0
+        # initial coarse sweep, sequential (parareal.py:265-270)
+        e0 = ev.start()
+        for i in range(N):
+            solver.run_G_batch(t_dev[i:i + 1], t_dev[i + 1:i + 2], UGk[i:i + 1], out=UGk[i + 1:i + 2])
+        ev.stop(e0, 'G')
+        Uk.copy_(UGk)
+        u[:, :, 0] = Uk.cpu().numpy()
+        G_time += ev.collect().get('G', 0.0)
+
+        cap = max(4 * N, 64)
+        Xd = torch.empty((cap, n), **f64)
+        Dd = torch.empty((cap, n), **f64)
+        rows = 0
+        k = 0
+        for k in range(N):
+            if verbose == 'v':
+                print(f'{self.ode_name} {model.name} iteration number (out of {N}): {k + 1} ')
+            e0 = ev.start()
+            self._fine_sweep(torch, t_dev, Uk, UF, I, N, n)
+            ev.stop(e0, 'F')
+            Uk1 = Uk.clone()
+            UGk1 = UGk.clone()
+            Uk1[I + 1] = UF[I + 1]            # u[I+1,:,k+1:] = uF[I+1,:,k]   (:331-333)
+            I = I + 1
+            # training data (:336-339): x += u[I-1:N,:,k]; D += uF[I:N+1,:,k] - uG[I:N+1,:,k]
+            new = N + 1 - I
+            if rows + new > Xd.shape[0]:
+                grow = max(2 * Xd.shape[0], rows + new)
+                Xd = torch.cat([Xd[:rows], torch.empty((grow - rows, n), **f64)])
+                Dd = torch.cat([Dd[:rows], torch.empty((grow - rows, n), **f64)])
+            Xd[rows:rows + new] = Uk[I - 1:N]
+            _lib.check(lib.nngp_parareal_update(new * n, UF[I:N + 1].data_ptr(), UGk[I:N + 1].data_ptr(),
+                                                None, Dd[rows:rows + new].data_ptr(), stream))
+            rows += new
+            d_new = Dd[rows - new:rows].cpu().numpy()
+            x = np.vstack([x, u[I - 1:N, :, k]])
+            D = np.vstack([D, d_new])
+            data_x[I - 1:N, :, k] = u[I - 1:N, :, k]
+            data_D[I - 1:N, :, k] = d_new
+            fe = ev.collect()
+            F_time += fe.get('F', 0.0)
+            F_time_serial += fe.get('F', 0.0)   # every slice runs for the whole launch
+
+            if I == N:                          # early stop (:343-348)
+                if verbose == 'v':
+                    print('WARNING: early stopping')
+                u[:, :, k + 1] = Uk1.cpu().numpy()
+                err[:, k] = np.linalg.norm(u[:, :, k + 1] - u[:, :, k], np.inf, 1)
+                err[-1, k] = np.nextafter(epsilon, 0)
+                break
+
+            model.fit_timed(x, D, k=k, data_x=data_x, data_y=data_D)
+            if is_nngp:
+                th0 = torch.tensor(model.draw_thetas(N - I), **f64)
+                nf = model.n_fits
+            e_loop = ev.start()
+            for i in range(I, N):
+                eg = ev.start()
+                solver.run_G_batch(t_dev[i:i + 1], t_dev[i + 1:i + 2], Uk1[i:i + 1], out=UGk1[i + 1:i + 2])
+                ev.stop(eg, 'G')
+                if is_nngp:
+                    j = i - I
+                    model.predict_device(Xd, Dd, rows, Uk1[i], th0[j * nf:(j + 1) * nf],
+                                         out=Uk1[i + 1], bias=UGk1[i + 1], stream=stream)
+                else:   # (uF - uG_prev) + uG_new   (models.py:82-83, parareal.py:382)
+                    _lib.check(lib.nngp_parareal_update(n, UF[i + 1].data_ptr(), UGk[i + 1].data_ptr(),
+                                                        UGk1[i + 1].data_ptr(), Uk1[i + 1].data_ptr(), stream))
+            ev.stop(e_loop, 'loop')
+            u[:, :, k + 1] = Uk1.cpu().numpy()
+            ug = UGk1.cpu().numpy()
+            te = ev.collect()
+            G_time += te.get('G', 0.0)
+            model.add_pred_time(max(te.get('loop', 0.0) - te.get('G', 0.0), 0.0))
+            if np.any(np.isnan(ug)):
+                raise Exception('NaN values in initial coarse solve - increase Ng!')
+            err[:, k] = np.linalg.norm(u[:, :, k + 1] - u[:, :, k], np.inf, 1)   # (:402-403)
+            err[I, k] = 0
+            II = I
+            for p in range(II + 1, N + 1):                                          # (:408-416)
+                if err[p, k] < epsilon:
+                    I = I + 1
+                else:
+                    break
+            if verbose == 'v':
+                print('--> Converged:', I)
+            conv_int.append(I)
+            Uk, UGk = Uk1, UGk1
+            if I == N:
+                break
+            if (early_stop is not None) and k == (early_stop - 1):
+                if verbose == 'v':
+                    print('Early stopping due to user condition.')
+                break
+
+        timings = {'F_time': F_time, 'G_time': G_time, 'F_time_serial_avg': F_time_serial}
+        timings.update(model.get_times())
+        return {'t': t, 'u': u[:, :, :k + 1], 'err': err[:, :k + 1], 'x': x, 'D': D, 'k': k + 1,
+                'data_x': data_x[..., :k + 1], 'data_D': data_D[..., :k + 1], 'timings': timings,
+                'debug_dict': {}, 'converged': I == N, 'conv_int': conv_int}

@@ -1,0 +1,83 @@
+"""CPU: host-side logic of the product package (no GPU calls)."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+
+def test_vectorised_draws_equal_the_reference_draw_loop():
+    """models.py:192 draws rng.integers(-8, 0, 2) once per fit; one vectorised call over a whole
+    iteration yields the same stream (power-of-two range: Lemire never rejects)."""
+    g = golden('rng.npz')['draws']
+    rng = np.random.default_rng(45)
+    assert np.array_equal(rng.integers(-8, 0, (len(g), 2)), g)
+
+
+def test_nngp_model_draw_order_matches_reference_predictions():
+    import nngp_amd
+    m = nngp_amd.NNGP_p(n=3, N=8, nn=10, seed=45)
+    a = m.draw_thetas(2)              # two consecutive predictions of 27 fits each
+    ref = np.random.default_rng(45)
+    exp = np.array([ref.integers(-8, 0, 2) for _ in range(54)], dtype=float)
+    assert np.array_equal(a, exp)
+    assert m.n_fits == 27 and m.maxfev == 400
+
+
+def test_adaptive_neighbours():
+    import nngp_amd
+    m = nngp_amd.NNGP_p(n=3, N=8, nn='adaptive')
+    m.k = 3
+    assert m.n_neighbours() == 10
+    m.k = 20
+    assert m.n_neighbours() == 22
+
+
+@pytest.mark.parametrize('key,factory', [
+    ('lorenz', lambda g: g.Lorenz(normalization='-11')),
+    ('hopf', lambda g: g.Hopf(normalization='-11')),
+    ('tomlab', lambda g: g.ThomasLabyrinth(normalization='-11')),
+    ('burgers128', lambda g: g.Burgers(d_x=128, normalization='-11')),
+    ('fhnpde10', lambda g: g.FHN_PDE(d_x=10)),
+    ('fhnpde10_n', lambda g: g.FHN_PDE(d_x=10, normalization='-11')),
+])
+def test_initial_conditions_match_reference(key, factory):
+    import nngp_amd
+    R = golden('rhs.npz')
+    assert np.array_equal(factory(nngp_amd).get_init_cond(), R[key + '__u0'])
+
+
+def test_normalisation_table():
+    import nngp_amd
+    o = nngp_amd.Lorenz(normalization='-11')
+    t = o.normalizer.device_table(3)
+    mn, mx = np.array([-17.1, -23, 6]), np.array([18.1, 25, 45])
+    assert np.array_equal(t, np.concatenate([mn, mx - mn, 2 / (mx - mn)]))
+    assert nngp_amd.Lorenz().normalizer.device_table(3) is None
+
+
+def test_configs_restate_reference():
+    import nngp_amd
+    c = nngp_amd.Config(nngp_amd.Lorenz(normalization='-11')).get()
+    assert (c['N'], c['Ng'], c['Nf'], c['G'], c['F']) == (50, 6, 450, 'RK4', 'RK4')
+    c = nngp_amd.Config(nngp_amd.Hopf(normalization='-11'), N=128).get()
+    assert (c['Ng'], c['Nf'], c['G'], c['F']) == (16, 1360, 'RK1', 'RK8')
+    c = nngp_amd.Config(nngp_amd.ThomasLabyrinth(normalization='-11'), N=256).get()
+    assert (c['Ng'], c['Nf'], c['tspan']) == (10, 3910, [0, 100])
+    c = nngp_amd.Config(nngp_amd.FHN_PDE(d_x=10), d_x=10).get()
+    assert (c['N'], c['Ng'], c['Nf'], c['G'], c['F'], c['tspan']) == (512, 3, 21, 'RK2', 'RK8', [0, 150])
+
+
+def test_paging_schedule_restates_solver_quirk():
+    from nngp_amd.solver import _paging_schedule
+    assert _paging_schedule(45, 10) == ([10, 10, 10, 10, 4], 44)
+    it, st = _paging_schedule(45, 7.3)
+    assert st == 44 and len(it) == 7 and abs(it[-1] - 44 % 7.3) < 1e-15
+
+
+def test_solver_rejects_unknown_tableau():
+    import nngp_amd
+    f = nngp_amd.Lorenz().get_vector_field()
+    with pytest.raises(NotImplementedError):
+        nngp_amd.SolverRK(f, 6, 45, 'RK3', 'RK4')
+    with pytest.raises(TypeError):
+        nngp_amd.SolverRK(lambda t, u: u, 6, 45, 'RK4', 'RK4')

@@ -1,0 +1,237 @@
+"""CPU: pin the oracle (oracle/nngp_oracle.c + oracle/oracle.py) against fixtures produced by running
+the reference itself (tests/golden/gen_golden.py).  No GPU needed.
+
+Tolerances (fp64):
+  * ODE right-hand sides and RK end states: bit-exact (same operation order as the reference);
+  * PDE right-hand sides: the reference sums dense rows in BLAS order -> |diff| <= 1e-12*max|f|;
+  * -LML: relative 1e-6 (ill-conditioned K with jitter 1e-20 amplifies Cholesky order);
+  * Nelder-Mead LOGIC: bit-exact vs scipy on the same objective (callback test);
+  * end-to-end: same iteration count K where K is roundoff-stable (Parareal, FHN nnGP);
+    chaotic Lorenz nnGP: K within +-2 of the reference.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+from scipy.optimize import minimize
+
+import oracle as O
+from conftest import golden
+from systems_table import EXACT, KEYS, RK_KEYS, oracle_system
+
+
+@pytest.mark.parametrize('key', KEYS)
+def test_rhs_matches_reference(key):
+    R = golden('rhs.npz')
+    s = oracle_system(key)
+    U, F = R[key + '__u'], R[key + '__f']
+    out = np.array([s.rhs(u) for u in U])
+    if key in EXACT:
+        assert np.array_equal(out, F)
+    else:
+        assert np.max(np.abs(out - F)) <= 1e-12 * max(1.0, np.max(np.abs(F)))
+
+
+@pytest.mark.parametrize('key', RK_KEYS)
+@pytest.mark.parametrize('tab', ['RK1', 'RK2', 'RK4', 'RK8'])
+def test_rk_matches_reference(key, tab):
+    R = golden('rk.npz')
+    s = oracle_system(key)
+    k = f'{key}__{tab}'
+    u0 = R[k + '__u0']
+    t0, t1, steps = R[k + '__span']
+    a = s.rk(int(tab[2:]), t0, t1, int(steps), u0, O.STEP_FIXED)
+    b = s.rk(int(tab[2:]), t0, t1, int(steps), u0, O.STEP_LINSPACE)
+    for got, ref in ((a, R[k + '__fixed']), (b, R[k + '__linspace'])):
+        if key in EXACT:
+            assert np.array_equal(got, ref)
+        else:
+            assert np.max(np.abs(got - ref)) <= 1e-14 * max(1.0, np.max(np.abs(ref)))
+
+
+def test_fixed_and_linspace_differ_only_by_roundoff():
+    s = oracle_system('lorenz')
+    u0 = np.array([-0.8, -0.6, -0.3])
+    a = s.rk(4, 0.0, 1.7, 37, u0, O.STEP_FIXED)
+    b = s.rk(4, 0.0, 1.7, 37, u0, O.STEP_LINSPACE)
+    assert np.max(np.abs(a - b)) < 1e-12
+
+
+@pytest.mark.parametrize('tag', ['paged', 'paged73'])
+def test_paging_quirk_matches_reference(tag):
+    R = golden('rk.npz')
+    s = oracle_system('lorenz')
+    t0, t1, steps, thresh = R[tag + '__lorenz__args']
+    thresh = thresh if tag == 'paged73' else int(thresh)
+    out = O.paged(lambda a, b, st, u: s.rk(4, a, b, st, u), t0, t1, int(steps), thresh, R['paged__lorenz__u0'])
+    assert np.array_equal(out, R[tag + '__lorenz__out'])
+
+
+def test_global_grid_is_the_linspace_grid():
+    s = oracle_system('lorenz')
+    u0 = np.array([-0.8, -0.6, -0.3])
+    whole = s.rk(1, 0.0, 0.37, 64, u0, O.STEP_LINSPACE)
+    x = u0
+    for i in range(8):
+        x = s.rk_grid(1, 0.0, 0.37, 64, 8 * i, 8, x)
+    assert np.all(np.isfinite(whole)) and np.array_equal(x, whole)
+
+
+def test_nlml_matches_reference():
+    L = golden('lml.npz')
+    D2 = O.d2_matrix(L['xm'])
+    v = np.array([[[O.nlml(D2, L['ym'][:, j], th, jit) for j in range(3)] for th in L['thetas']]
+                  for jit in L['jitters']])
+    ref = L['nlml']
+    assert np.array_equal(np.isinf(v), np.isinf(ref))
+    both = np.isfinite(v) & np.isfinite(ref)
+    rel = np.abs(v[both] - ref[both]) / np.maximum(1, np.abs(ref[both]))
+    assert rel.max() < 1e-6
+    assert np.median(rel) < 1e-14
+
+
+def test_nlml_singular_kernel_failure_semantics():
+    """Duplicated rows: K is singular without jitter; a failed Cholesky is +inf (models.py:250)."""
+    L = golden('lml.npz')
+    D2 = O.d2_matrix(L['xd'])
+    v = np.array([[O.nlml(D2, L['yd'][:, 0], th, jit) for th in L['thetas']] for jit in L['jitters']])
+    ref = L['nlml_dup']
+    agree = (np.isinf(v) == np.isinf(ref)).mean()
+    assert agree > 0.99          # pass/fail flips only at the numerical edge of positive-definiteness
+    both = np.isfinite(v) & np.isfinite(ref)
+    rel = np.abs(v[both] - ref[both]) / np.maximum(1, np.abs(ref[both]))
+    assert np.median(rel) < 1e-10
+
+
+def test_posterior_mean_matches_reference():
+    L = golden('lml.npz')
+    pm = np.array([[O.gp_mean(L['xm'], L['ym'][:, j], L['new_x'], th, -15.0) for j in range(3)]
+                   for th in L['thetas']])
+    ref = L['post_mean_jit15']
+    assert np.array_equal(np.isnan(pm), np.isnan(ref))
+    assert np.nanmax(np.abs(pm - ref)) < 1e-8
+
+
+# --------------------------------------------------------------------------------------------
+# Nelder-Mead: the C restatement vs scipy on the SAME objective -> bit-exact
+# --------------------------------------------------------------------------------------------
+_CB = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.POINTER(ctypes.c_double), ctypes.c_void_p)
+
+
+def _c_nm(fn, th0, fatol, xatol, maxfev):
+    L = O.lib()
+    L.orc_nm_core.argtypes = [_CB, ctypes.c_void_p, O._dp, ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                              O._dp, O._dp, ctypes.POINTER(ctypes.c_int)]
+    cb = _CB(lambda x, ctx: float(fn(np.array([x[0], x[1]]))))
+    th0 = np.ascontiguousarray(th0, dtype=float)
+    th = np.empty(2)
+    fv = np.empty(1)
+    ne = ctypes.c_int()
+    L.orc_nm_core(cb, None, O._p(th0), fatol, xatol, maxfev, O._p(th), O._p(fv), ctypes.byref(ne))
+    return th, fv[0], ne.value
+
+
+def _objectives():
+    L = golden('nm.npz')
+    xm, ym = L['m10__xm'], L['m10__ym']
+    D2 = O.d2_matrix(xm)
+    yield 'lml', lambda th: O.nlml(D2, ym[:, 0], th, -15.0)
+    yield 'lml_jit20', lambda th: O.nlml(D2, ym[:, 2], th, -20.0)
+    yield 'rosen', lambda th: (1 - th[0]) ** 2 + 100 * (th[1] - th[0] ** 2) ** 2
+    yield 'inf_region', lambda th: np.inf if th[0] + th[1] > -3 else (th[0] + 2) ** 2 + (th[1] + 4) ** 4
+    yield 'flat', lambda th: 1.0
+
+
+@pytest.mark.parametrize('maxfev', [400, 7, 12])
+def test_nelder_mead_logic_bit_exact_vs_scipy(maxfev):
+    rng = np.random.default_rng(0)
+    for name, fn in _objectives():
+        for _ in range(6):
+            th0 = rng.integers(-8, 0, 2).astype(float)
+            for tol in (0.1, 1e-3):
+                ref = minimize(fn, th0, method='Nelder-Mead',
+                               options={'fatol': tol, 'xatol': tol, 'maxfev': maxfev, 'maxiter': maxfev})
+                th, fv, ne = _c_nm(fn, th0, tol, tol, maxfev)
+                assert ne == ref.nfev, name
+                assert np.array_equal(th, ref.x), name
+                assert fv == ref.fun or (np.isinf(fv) and np.isinf(ref.fun)), name
+
+
+def test_nm_fits_track_reference():
+    """Full fits on the reference -LML.  Per-fit iterates are NOT pinned (roundoff in the
+    -LML redirects NM in flat directions); the optimum value mostly agrees."""
+    N = golden('nm.npz')
+    agree = []
+    for tag in ['m10', 'm18tol3', 'm30']:
+        xm, ym, ins, th0, tol, out = [N[tag + '__' + k] for k in ['xm', 'ym', 'ins', 'th0', 'tol', 'out']]
+        D2 = O.d2_matrix(xm)
+        for q, (j, jit) in enumerate(ins):
+            th, fv, ne = O.nm_fit(D2, ym[:, int(j)], th0[q], jit, tol[0], tol[1])
+            agree.append(abs(fv - out[q, 2]) <= 1e-6 * max(1, abs(out[q, 2])))
+    assert np.mean(agree) > 0.9
+
+
+def test_knn_matches_reference_up_to_exact_ties():
+    K = golden('knn.npz')
+    idx, dist = O.knn(K['X'], K['q'], K['X'].shape[0])   # full ordering, incl. the 7/100 tie
+    ref = K['idx']
+    assert np.array_equal(dist, K['dist'][ref])          # same distances, same order
+    for a, b in zip(idx, ref):
+        assert a == b or K['dist'][a] == K['dist'][b]     # only exact ties may permute
+    assert idx[list(idx).index(7)] == 7 and (100 in idx)  # tie broken by row index (7 before 100)
+    assert list(idx).index(7) < list(idx).index(100)
+
+
+def test_predict_d128_matches_reference():
+    """One NNGP_p.predict at d=128, m=15 (1152 fits) on Parareal-like data."""
+    P = golden('preds_d128.npz')
+    rng = np.random.default_rng(int(P['seed']))
+    th0 = rng.integers(-8, 0, (1152, 2)).astype(float)
+    assert np.array_equal(th0, P['rnd'])                  # the reference's draw order (models.py:192)
+    idx, _ = O.knn(P['X'], P['new_x'], int(P['m']))
+    assert np.array_equal(P['X'][idx], P['xm'])           # same neighbours, same order
+    preds, fits = O.predict(P['X'], P['Y'], P['new_x'], int(P['m']), th0, return_fits=True)
+    ref = P['preds']
+    assert np.max(np.abs(preds - ref)) <= 1e-8 * np.max(np.abs(ref))
+    r = P['fit_res']
+    assert np.mean(np.abs(fits[:, 2] - r[:, 2]) <= 1e-6 * np.maximum(1, np.abs(r[:, 2]))) > 0.9
+
+
+# --------------------------------------------------------------------------------------------
+# end to end
+# --------------------------------------------------------------------------------------------
+def test_parareal_lorenz_matches_reference():
+    """BASELINE configs[0] (Lorenz N=32, G=F=RK4 6/450 steps per slice): Parareal K and iterates."""
+    P = golden('para_lorenz.npz')
+    s = O.System('lorenz')
+    r = O.parareal(s, [0, 18], 32, 6, 450, 'RK4', 'RK4', model='parareal', u0=s.fit([-15, -15, 20]))
+    assert r['k'] == int(P['para__k'])
+    assert r['conv_int'] == list(P['para__conv_int'])
+    assert np.nanmax(np.abs(r['u'] - P['para__u'])) < 1e-9
+
+
+def test_nngp_lorenz_seed_k_within_chaos_spread():
+    P = golden('para_lorenz.npz')
+    s = O.System('lorenz')
+    ks = []
+    for seed in (45, 47):
+        r = O.parareal(s, [0, 18], 32, 6, 450, 'RK4', 'RK4', model='nngp', nn=10, seed=seed,
+                       u0=s.fit([-15, -15, 20]))
+        ks.append(r['k'])
+        assert abs(r['k'] - int(P[f'nngp_s{seed}__k'])) <= 2
+        assert r['converged']
+
+
+def test_fhn_ode_parareal_and_nngp_match_reference():
+    P = golden('para_fhn.npz')
+    s = O.System('fhn_ode')
+    u0 = s.fit([-1, 1])
+    r = O.parareal(s, [0, 40], 40, 4, 4000, 'RK2', 'RK4', model='parareal', u0=u0)
+    assert r['k'] == int(P['para__k'])
+    assert np.nanmax(np.abs(r['u'] - P['para__u'])) < 1e-9
+    r = O.parareal(s, [0, 40], 40, 4, 4000, 'RK2', 'RK4', model='nngp', nn=15, seed=45, u0=u0)
+    assert r['k'] == int(P['nngp_s45__k'])
+    assert r['conv_int'] == list(P['nngp_s45__conv_int'])
+    # intermediate iterates carry GP roundoff (NM branch flips); the converged column does not
+    assert np.nanmax(np.abs(r['u'] - P['nngp_s45__u'])) < 1e-3
+    assert np.max(np.abs(r['u'][:, :, -1] - P['nngp_s45__u'][:, :, -1])) < 1e-8
