@@ -1,0 +1,226 @@
+"""bench.py -- nnGParareal hot path on MI355X.
+
+Metric (BASELINE.json): fine RK steps/sec + nnGP corrections/sec; wall-clock to convergence (K).
+Workload at N=1 (BASELINE.json configs[1]): non-autonomous Hopf, N=128 time slices, RK4 fine
+solver with Hopf.py's throughput schedule (Nf = 2048*85*10^4 -> 13.6e6 steps per slice, unpaged),
+G = RK1 16 steps/slice, nnGP m=15, 2 restarts, fatol = xatol = 0.1, eps = 5e-7 (Hopf.py:65-84).
+
+One timed "step" = one Parareal fine sweep: every slice propagated by the batched HIP RK kernel
+(inputs resident in HBM), followed -- for N>1 -- by the single RCCL all-gather of the fine end
+states.  Weak scaling: every rank owns 128 slices, so the job integrates 128*N slices per step.
+value = (slices x fine steps per slice, all ranks) / max-over-ranks wall time of the K steps.
+
+Also reported (rank 0): nnGP corrections/s (the sequential correction sweep of one iteration on
+the same config), wall-clock to convergence with its K for the full nnGParareal solve of the
+Hopf config and of the Burgers d=128 N=128 config (BASELINE configs[2], the north star's 10x
+target), the FP64-VALU roofline of the fine kernel (HIP events around the launches), and the CPU
+baseline: the oracle's C restatement (OpenMP over slices) on a bounded sample of the same sweep.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector: half the 157.3 TF FP32 vector peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+# algorithmic flops per fine step per slice: S*F_rhs + (2 nnz(a) + S + 2 nnz(b))*d
+FLOPS_PER_STEP = {('hopf', 'RK4'): 126, ('hopf', 'RK8'): 11 * 18 + (2 * 39 + 11 + 2 * 5) * 3,
+                  ('burgers', 'RK8'): 28160}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_init():
+    import torch
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group('nccl', device_id=torch.device('cuda', local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank
+
+
+def barrier_sync(torch, world):
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+
+
+def hopf_setup(g, steps_per_slice, n_slices):
+    ode = g.Hopf(normalization='-11')
+    solver = g.SolverRK(ode.get_vector_field(), Ng=2048 // 128, Nf=steps_per_slice, F='RK4', G='RK1',
+                        thresh=float('inf'))
+    return ode, solver
+
+
+def fine_sweep_bench(torch, g, world, rank, steps, warmup, steps_per_slice, slices_per_rank):
+    """Time K fine sweeps of 128*world slices (weak scaling), HIP events around the kernel."""
+    n_total = slices_per_rank * world
+    ode, solver = hopf_setup(g, steps_per_slice, n_total)
+    rng = np.random.default_rng(1234)
+    # synthetic initial data: states uniformly inside the normalised box, times along [-20, 500]
+    t = np.linspace(-20, 500, n_total + 1)
+    U = rng.uniform(-0.5, 0.5, size=(n_total, 3))
+    dev = lambda a: torch.tensor(a, dtype=torch.float64, device='cuda')
+    lo, hi = rank * slices_per_rank, (rank + 1) * slices_per_rank
+    t0, t1, u0 = dev(t[lo:hi]), dev(t[lo + 1:hi + 1]), dev(U[lo:hi])
+    out = torch.empty_like(u0)
+    gathered = torch.empty((n_total, 3), dtype=torch.float64, device='cuda')
+    ev = []
+
+    def one(record):
+        if record:
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record()
+        solver.run_F_batch(t0, t1, u0, out=out)
+        if record:
+            b.record()
+            ev.append((a, b))
+        if world > 1:
+            torch.distributed.all_gather_into_tensor(gathered, out)
+
+    for _ in range(warmup):
+        one(False)
+    barrier_sync(torch, world)
+    t_start = time.perf_counter()
+    for _ in range(steps):
+        one(True)
+    barrier_sync(torch, world)
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kernel_s = np.mean([a.elapsed_time(b) / 1e3 for a, b in ev])
+    return elapsed, kernel_s, n_total, out
+
+
+def corrections_bench(torch, g, m=15, R=2, n_slices=128):
+    """One iteration's sequential nnGP correction sweep on Hopf-config training data."""
+    ode = g.Hopf(normalization='-11')
+    solver = g.SolverRK(ode.get_vector_field(), Ng=16, Nf=1360, F='RK4', G='RK1')
+    p = g.Parareal(ode, solver, [-20, 500], n_slices, epsilon=5e-7, verbose=None)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r = p.run(model='nngp', nn=m, n_restarts=R, fatol=0.1, xatol=0.1, seed=45, early_stop=2)
+    torch.cuda.synchronize()
+    # predictions per iteration = N - I with I the first unconverged slice after the F sweep
+    n_pred = sum(n_slices - i for i in [1] + [c + 1 for c in r['conv_int'][:-1]])
+    return n_pred, r['timings']['mdl_pred_t'], time.perf_counter() - t0
+
+
+def converge(torch, g, which):
+    if which == 'hopf':
+        ode = g.Hopf(normalization='-11')
+        solver = g.SolverRK(ode.get_vector_field(), Ng=16, Nf=2048 * 85 * 10000 // 128, F='RK4', G='RK1',
+                            thresh=float('inf'))
+        p = g.Parareal(ode, solver, [-20, 500], 128, epsilon=5e-7, verbose=None)
+        kw = dict(nn=15, n_restarts=2, fatol=0.1, xatol=0.1, seed=45)
+    else:   # Burgers_perf_across_m.py:30-33 (d=128, N=128, T=5, Nf/N=2000 RK8, Ng/N=4 RK1), m=15
+        ode = g.Burgers(d_x=128, normalization='-11')
+        solver = g.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
+        p = g.Parareal(ode, solver, [0, 5], 128, epsilon=5e-7, verbose=None)
+        kw = dict(nn=15, seed=45)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r = p.run(model='nngp', **kw)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, r['k'], r['converged'], r['timings']
+
+
+def cpu_baseline(steps_per_slice_full, n_slices, target_s=10.0):
+    """Oracle C restatement (OpenMP over slices) on a bounded sample of the fine sweep."""
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import oracle as O
+    threads = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or len(os.sched_getaffinity(0))
+    s = O.System('hopf', param=(500.0,))
+    rng = np.random.default_rng(1234)
+    U = rng.uniform(-0.5, 0.5, size=(n_slices, 3))
+    t = np.linspace(-20, 500, n_slices + 1)
+    probe = 20000
+    t0 = time.perf_counter()
+    s.rk_batch(4, t[:-1], t[1:], probe, U, nthreads=threads)
+    dt = time.perf_counter() - t0
+    steps = int(min(steps_per_slice_full, max(probe, probe * target_s / max(dt, 1e-6))))
+    t0 = time.perf_counter()
+    s.rk_batch(4, t[:-1], t[1:], steps, U, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {'value': n_slices * steps / dt, 'unit': 'fine RK steps/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{n_slices} Hopf slices x {steps} RK4 steps (of {steps_per_slice_full}), '
+                      f'{dt:.1f} s, oracle/nngp_oracle.c -O2 OpenMP'}
+
+
+def read_traffic():
+    path = os.path.join(ROOT, 'profiles', 'fine_kernel_traffic.json')
+    if os.path.exists(path):
+        try:
+            return json.load(open(path)).get('bytes_per_launch')
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--steps-per-slice', type=int, default=2048 * 85 * 10000 // 128)   # 13.6e6
+    ap.add_argument('--slices-per-gpu', type=int, default=128)
+    ap.add_argument('--no-extras', action='store_true', help='skip corrections/convergence/CPU legs')
+    args = ap.parse_args()
+
+    import torch
+    world, rank = dist_init()
+    import nngp_amd as g
+    g.lib()
+
+    elapsed, kernel_s, n_total, _ = fine_sweep_bench(torch, g, world, rank, args.steps, args.warmup,
+                                                     args.steps_per_slice, args.slices_per_gpu)
+    total_steps = n_total * args.steps_per_slice * args.steps
+    value = total_steps / elapsed
+    flops_launch = FLOPS_PER_STEP[('hopf', 'RK4')] * args.steps_per_slice * args.slices_per_gpu
+    achieved_tf = flops_launch / kernel_s / 1e12
+    res = {
+        'metric': 'fine RK steps/sec (+ nnGP corrections/sec; wall-clock to convergence)',
+        'value': value, 'unit': 'fine RK steps/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': elapsed / args.steps * 1e3, 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
+        'config': {'workload': 'nonautonomous Hopf (Hopf.py), RK4 fine sweep, 13.6e6 steps/slice',
+                   'slices_per_gpu': args.slices_per_gpu, 'total_slices': n_total,
+                   'steps_per_slice': args.steps_per_slice, 'parallelism': f'time-slices x{world}'},
+        'roofline': {'bound': 'fp64-valu', 'achieved': achieved_tf, 'peak': FP64_PEAK_TFLOPS,
+                     'unit': 'TFLOP/s', 'frac': achieved_tf / FP64_PEAK_TFLOPS, 'traffic': read_traffic(),
+                     'kernel': 'rk_lane_kernel<HOPF,RK4>', 'kernel_ms': kernel_s * 1e3,
+                     'flops_per_step_per_slice': FLOPS_PER_STEP[('hopf', 'RK4')]},
+    }
+    if rank == 0 and world == 1 and not args.no_extras:
+        n_pred, pred_s, _ = corrections_bench(torch, g)
+        res['nngp_corrections_per_s'] = n_pred / pred_s
+        res['nngp_correction_ms'] = pred_s / n_pred * 1e3
+        for which in ('burgers', 'hopf'):
+            wall, k, conv, tim = converge(torch, g, which)
+            res[f'{which}_n128_to_convergence'] = {'wall_s': wall, 'K': k, 'converged': conv,
+                                                   'F_time_s': tim['F_time'], 'mdl_time_s': tim['mdl_tot_t']}
+            log(which, 'converged', conv, 'K', k, f'{wall:.2f}s')
+        res['cpu_baseline'] = cpu_baseline(args.steps_per_slice, args.slices_per_gpu)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -36,6 +36,7 @@ class VectorField:
             p = (ctypes.c_double * 4)(*(list(ode.param) + [0.0] * (4 - len(ode.param))))
             cs = _lib.CSystem(ode.kind, ode.d, ode.nx, int(ode.normalized), p,
                               norm_t.data_ptr() if norm_t is not None else None)
+            cs._keep_alive = norm_t   # the struct holds a raw device pointer into this tensor
             self._dev[key] = (cs, norm_t)
         return self._dev[key][0]
 
