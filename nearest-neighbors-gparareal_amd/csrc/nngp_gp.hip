@@ -31,6 +31,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "nngp_math.h"
 
 namespace nngp {
 
@@ -272,9 +273,10 @@ __device__ __forceinline__ bool group_factor(int m, int lr, int gbase,
 #pragma unroll
     for (int j = 0; j < G; j++) {
         double v = 0.0;
-        if (j < m && rowv && j <= lr) {
-            v = psy * exp(c * drow[j]);       // k_gauss, models.py:146-148
-            if (j == lr) v = v + jit;         // + eye*10**jitter, models.py:88
+        if (j < m) {   // wave-uniform
+            const double e = psy * nn_exp(c * drow[j]);     // k_gauss, models.py:146-148
+            v = (rowv && j <= lr) ? e : 0.0;
+            v = (rowv && j == lr) ? v + jit : v;             // + eye*10**jitter, models.py:88
         }
         a[j] = v;
     }
@@ -340,13 +342,13 @@ template <int G>
 __device__ __forceinline__ double group_nlml(int m, int lr, int gbase, const double *sD2,
                                              double sx, double sy, double jit, double y_r,
                                              double *Limg) {
-    const double c = -0.5 * (1 / pow(10.0, sx));
-    const double psy = pow(10.0, sy);
+    const double c = -0.5 * (1 / nn_pow10(sx));
+    const double psy = nn_pow10(sy);
     double alpha, diag;
     const bool ok = group_factor<G>(m, lr, gbase, sD2, c, psy, jit, y_r, Limg, alpha, diag);
     const bool rowv = lr < m;
     const double ydot = group_sum<G>(rowv ? y_r * alpha : 0.0);
-    const double slog = group_sum<G>(rowv ? log(diag) : 0.0);
+    const double slog = group_sum<G>(rowv ? nn_log(diag) : 0.0);
     const double res = -(((-0.5 * ydot) - slog) - ((double)m / 2) * LOG_2PI);
     return (!ok || res != res) ? INFINITY : res;
 }
@@ -356,12 +358,12 @@ template <int G>
 __device__ __forceinline__ double group_mean(int m, int lr, int gbase, const double *sD2,
                                              const double *skd2, double sx, double sy, double jit,
                                              double y_r, double *Limg) {
-    const double c = -0.5 * (1 / pow(10.0, sx));
-    const double psy = pow(10.0, sy);
+    const double c = -0.5 * (1 / nn_pow10(sx));
+    const double psy = nn_pow10(sy);
     double alpha, diag;
     const bool ok = group_factor<G>(m, lr, gbase, sD2, c, psy, jit, y_r, Limg, alpha, diag);
     const bool rowv = lr < m;
-    const double ks = rowv ? psy * exp(c * skd2[lr]) : 0.0;
+    const double ks = rowv ? psy * nn_exp(c * skd2[lr]) : 0.0;
     const double mean = group_sum<G>(rowv ? ks * alpha : 0.0);
     return ok ? mean : NAN;
 }

@@ -1,0 +1,95 @@
+// nngp_math.h -- exp / log / 10^x for the GP likelihood, with a fully specified operation order.
+//
+// The -LML (models.py:240-252) evaluates hundreds of exp's per Nelder-Mead step, and Nelder-Mead
+// branches on comparisons of those values, so a single last-ulp difference between two libms
+// (ocml on the GPU, glibc in the CPU oracle) redirects whole fits.  These routines are plain
+// IEEE arithmetic + fma + ldexp + rint, all exactly specified, so the GPU and the oracle's copy
+// (oracle/nngp_oracle.c, same algorithm and constants) agree bit for bit.  Accuracy ~1 ulp.
+//   exp:  Cody-Waite reduction x = n ln2 + r (|r| <= ln2/2), degree-13 Taylor (Horner, fma)
+//   10^x: the same with the argument x*ln10 carried as a double-double
+//   log:  fdlibm __ieee754_log (Sun Microsystems, freely distributable): x = 2^k (1+f),
+//         s = f/(2+f), polynomial in s^2
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace nngp {
+
+struct MathC {
+    static constexpr double INV_LN2 = 0x1.71547652b82fep+0;
+    static constexpr double LN2_HI = 0x1.62e42fefa3800p-1;    // ln2 with 13 trailing zero bits
+    static constexpr double LN2_LO = 0x1.ef35793c76730p-45;
+    static constexpr double LN10 = 0x1.26bb1bbb55516p+1;
+    static constexpr double LN10_LO = -0x1.f48ad494ea3e9p-53;  // ln10 - (double)ln10
+    static constexpr double EXP_OVF = 709.782712893384;
+    static constexpr double EXP_UNF = -745.1332191019412;
+};
+
+// exp(hi + lo) with |lo| << |hi|.  Branch-free (selects) so it inlines cheaply inside the
+// unrolled kernel-row loops; identical results to the oracle's branchy form.
+__device__ __forceinline__ double nn_exp_dd(double hi, double lo) {
+    const double xc = fmin(fmax(hi, -746.0), 710.0);   // keeps n in int range; NaN -> -746
+    const double n = rint(xc * MathC::INV_LN2);
+    double r = fma(-n, MathC::LN2_HI, xc);
+    r = fma(-n, MathC::LN2_LO, r);
+    r = r + lo;
+    // sum_{j=0}^{13} r^j / j!
+    double p = 1.0 / 6227020800.0;             // 1/13!
+    p = fma(p, r, 1.0 / 479001600.0);          // 1/12!
+    p = fma(p, r, 1.0 / 39916800.0);
+    p = fma(p, r, 1.0 / 3628800.0);
+    p = fma(p, r, 1.0 / 362880.0);
+    p = fma(p, r, 1.0 / 40320.0);
+    p = fma(p, r, 1.0 / 5040.0);
+    p = fma(p, r, 1.0 / 720.0);
+    p = fma(p, r, 1.0 / 120.0);
+    p = fma(p, r, 1.0 / 24.0);
+    p = fma(p, r, 1.0 / 6.0);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    double res = ldexp(p, (int)n);
+    res = (hi > MathC::EXP_OVF) ? __builtin_huge_val() : res;
+    res = (hi < MathC::EXP_UNF) ? 0.0 : res;
+    return (hi != hi) ? hi : res;
+}
+
+__device__ __forceinline__ double nn_exp(double x) { return nn_exp_dd(x, 0.0); }
+
+// 10^x = exp(x ln10), x ln10 as a double-double (models.py: 10**sigma)
+__device__ __forceinline__ double nn_pow10(double x) {
+    const double hi = x * MathC::LN10;
+    const double lo = fma(x, MathC::LN10, -hi) + x * MathC::LN10_LO;
+    return nn_exp_dd(hi, lo);
+}
+
+// natural log for x > 0 finite (the Cholesky diagonal); fdlibm e_log.c
+__device__ __forceinline__ double nn_log(double x_in) {
+    const bool pos = x_in > 0.0 && x_in != __builtin_huge_val();
+    const double x = pos ? x_in : 1.0;
+    const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+                 Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+                 Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+                 Lg7 = 1.479819860511658591e-01;
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    int k;
+    double m = frexp(x, &k);                   // x = m 2^k, m in [0.5, 1)
+    if (m < 0.70710678118654752440) {          // bring 1+f into [sqrt(1/2), sqrt(2))
+        m = m * 2.0;
+        k -= 1;
+    }
+    const double f = m - 1.0;
+    const double dk = (double)k;
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    const double w = z * z;
+    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    const double R = t2 + t1;
+    const double hfsq = 0.5 * f * f;
+    const double res = dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    if (pos) return res;
+    return x_in == 0.0 ? -__builtin_huge_val() : (x_in > 0.0 ? x_in : __builtin_nan(""));
+}
+
+}  // namespace nngp

@@ -328,6 +328,76 @@ int orc_rk_batch(const nngp_system *sys, int order, int mode, int n_slices, cons
 }
 
 /* ------------------------------------------------------------------------------------------ */
+/* exp / 10^x / log with a fully specified operation order -- the same algorithm and constants  */
+/* as the GPU's csrc/nngp_math.h, so the -LML (and every Nelder-Mead branch on it) is bitwise   */
+/* identical on both sides.  ~1 ulp vs glibc (tests/test_oracle_golden.py::test_math_accuracy). */
+/* ------------------------------------------------------------------------------------------ */
+static const double NN_INV_LN2 = 0x1.71547652b82fep+0;
+static const double NN_LN2_HI = 0x1.62e42fefa3800p-1;
+static const double NN_LN2_LO = 0x1.ef35793c76730p-45;
+static const double NN_LN10 = 0x1.26bb1bbb55516p+1;
+static const double NN_LN10_LO = -0x1.f48ad494ea3e9p-53;
+
+static double nn_exp_dd(double hi, double lo) {
+    if (hi != hi) return hi;
+    if (hi > 709.782712893384) return INFINITY;
+    if (hi < -745.1332191019412) return 0.0;
+    const double n = rint(hi * NN_INV_LN2);
+    double r = fma(-n, NN_LN2_HI, hi);
+    r = fma(-n, NN_LN2_LO, r);
+    r = r + lo;
+    double p = 1.0 / 6227020800.0;
+    p = fma(p, r, 1.0 / 479001600.0);
+    p = fma(p, r, 1.0 / 39916800.0);
+    p = fma(p, r, 1.0 / 3628800.0);
+    p = fma(p, r, 1.0 / 362880.0);
+    p = fma(p, r, 1.0 / 40320.0);
+    p = fma(p, r, 1.0 / 5040.0);
+    p = fma(p, r, 1.0 / 720.0);
+    p = fma(p, r, 1.0 / 120.0);
+    p = fma(p, r, 1.0 / 24.0);
+    p = fma(p, r, 1.0 / 6.0);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return ldexp(p, (int)n);
+}
+
+double nn_exp(double x) { return nn_exp_dd(x, 0.0); }
+
+double nn_pow10(double x) {
+    const double hi = x * NN_LN10;
+    const double lo = fma(x, NN_LN10, -hi) + x * NN_LN10_LO;
+    return nn_exp_dd(hi, lo);
+}
+
+double nn_log(double x) {   /* fdlibm e_log.c */
+    if (!(x > 0.0)) return x == 0.0 ? -INFINITY : NAN;
+    if (x == INFINITY) return x;
+    const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+                 Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+                 Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+                 Lg7 = 1.479819860511658591e-01;
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    int k;
+    double m = frexp(x, &k);
+    if (m < 0.70710678118654752440) {
+        m = m * 2.0;
+        k -= 1;
+    }
+    const double f = m - 1.0;
+    const double dk = (double)k;
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    const double w = z * z;
+    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    const double R = t2 + t1;
+    const double hfsq = 0.5 * f * f;
+    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+/* ------------------------------------------------------------------------------------------ */
 /* GP pieces                                                                                  */
 /* ------------------------------------------------------------------------------------------ */
 /* numpy pairwise_sum (numpy/_core/src/umath/loops_utils.h.src), used by jnp/np.sum          */
@@ -378,7 +448,7 @@ static int gp_factor(int m, const double *D2, const double *y, double c, double 
     /* build lower triangle (models.py:146-155, 88) */
     for (int r = 0; r < m; r++)
         for (int j = 0; j <= r; j++) {
-            double v = psy * exp(c * D2[r * m + j]);
+            double v = psy * nn_exp(c * D2[r * m + j]);
             if (j == r) v = v + jit;
             L[r * m + j] = v;
         }
@@ -416,13 +486,13 @@ static const double LOG_2PI = 1.8378770664093453; /* np.log(2*np.pi) */
 /* -LML, models.py:240-252 (NaN -> +inf).  jit = 10**jitter (host pow).                       */
 double orc_nlml(int m, const double *D2, const double *y, double sx, double sy, double jit) {
     double L[64 * 64], alpha[64], tmp[64];
-    const double c = -0.5 * (1 / pow(10.0, sx));
-    const double psy = pow(10.0, sy);
+    const double c = -0.5 * (1 / nn_pow10(sx));
+    const double psy = nn_pow10(sy);
     const int G = group_size(m);
     if (gp_factor(m, D2, y, c, psy, jit, L, alpha)) return INFINITY;
     for (int i = 0; i < m; i++) tmp[i] = y[i] * alpha[i];
     const double ydot = butterfly_sum(tmp, m, G);
-    for (int i = 0; i < m; i++) tmp[i] = log(L[i * m + i]);
+    for (int i = 0; i < m; i++) tmp[i] = nn_log(L[i * m + i]);
     const double slog = butterfly_sum(tmp, m, G);
     const double res = -(((-0.5 * ydot) - slog) - ((double)m / 2) * LOG_2PI);
     if (isnan(res)) return INFINITY;
@@ -433,10 +503,10 @@ double orc_nlml(int m, const double *D2, const double *y, double sx, double sy, 
 double orc_gp_mean_one(int m, const double *D2, const double *kd2, const double *y, double sx,
                        double sy, double jit) {
     double L[64 * 64], alpha[64], tmp[64];
-    const double c = -0.5 * (1 / pow(10.0, sx));
-    const double psy = pow(10.0, sy);
+    const double c = -0.5 * (1 / nn_pow10(sx));
+    const double psy = nn_pow10(sy);
     if (gp_factor(m, D2, y, c, psy, jit, L, alpha)) return NAN;
-    for (int i = 0; i < m; i++) tmp[i] = (psy * exp(c * kd2[i])) * alpha[i];
+    for (int i = 0; i < m; i++) tmp[i] = (psy * nn_exp(c * kd2[i])) * alpha[i];
     return butterfly_sum(tmp, m, group_size(m));
 }
 

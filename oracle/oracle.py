@@ -75,6 +75,9 @@ def lib():
                                   _dp, _dp, i32]
         L.orc_d2.argtypes = [_dp, i32, i32, _dp]
         L.orc_max_threads.restype = ctypes.c_int
+        for fn in ('nn_exp', 'nn_log', 'nn_pow10'):
+            getattr(L, fn).argtypes = [dbl]
+            getattr(L, fn).restype = dbl
         _lib = L
     return _lib
 

@@ -167,7 +167,7 @@ def test_nm_fit_batch_vs_oracle(gpu, m, d, tol):
         exact += same
         if not same:   # an ulp in exp/log/pow may redirect NM; the optimum value must still agree
             assert abs(fv - res['fval'][f]) <= 1e-6 * max(1.0, abs(fv)) or np.isinf(fv) == np.isinf(res['fval'][f])
-    assert exact >= 0.9 * len(coords)
+    assert exact == len(coords)   # shared exp/log/10^x: bitwise
 
 
 def test_gp_mean_vs_oracle(gpu):
@@ -194,7 +194,7 @@ def test_predict_d128_vs_oracle_and_reference(gpu):
                                fits_out=fits).cpu().numpy()
     ora, ofits = O.predict(P['X'], P['Y'], P['new_x'], 15, th0, return_fits=True)
     f = fits.cpu().numpy()
-    assert (np.all(f == ofits, axis=1)).mean() > 0.95
+    assert np.array_equal(f, ofits)
     assert np.max(np.abs(preds - ora)) <= 1e-12 * np.max(np.abs(ora))
     assert np.max(np.abs(preds - P['preds'])) <= 1e-8 * np.max(np.abs(P['preds']))
 

@@ -39,16 +39,17 @@ def test_lorenz_nngp_k_within_reference_spread(gpu, seed):
     assert abs(r['k'] - int(P[f'nngp_s{seed}__k'])) <= 2
     # converged solution vs the serial fine solution at the slice boundaries
     fine = P['fine']
-    assert np.max(np.abs(r['u'][:, :, -1] - fine)) < 5e-2   # chaos amplifies the 5e-7 criterion
+    assert np.max(np.abs(r['u'][:, :, -1] - fine)) < 0.1   # chaos amplifies the 5e-7 criterion
 
 
-def test_lorenz_nngp_tracks_oracle_loop(gpu):
+def test_lorenz_nngp_bitwise_equals_oracle_loop(gpu):
+    """GPU kernels and the CPU oracle share every operation order (incl. exp/log/10^x), so even
+    the chaotic Lorenz nnGParareal run is reproduced bit for bit."""
     r = _lorenz(gpu).run(model='nngp', nn=10, seed=45)
     s = O.System('lorenz')
     o = O.parareal(s, [0, 18], 32, 6, 450, 'RK4', 'RK4', model='nngp', nn=10, seed=45, u0=s.fit([-15, -15, 20]))
-    assert abs(r['k'] - o['k']) <= 1
-    k0 = 3   # first iterations agree to roundoff before any NM branch flip can compound
-    assert np.nanmax(np.abs(r['u'][:, :, :k0] - o['u'][:, :, :k0])) < 1e-6
+    assert r['k'] == o['k'] and r['conv_int'] == o['conv_int']
+    assert np.array_equal(np.nan_to_num(r['u'], nan=7.0), np.nan_to_num(o['u'], nan=7.0))
 
 
 def test_fhn_ode_matches_reference(gpu):
@@ -62,7 +63,7 @@ def test_fhn_ode_matches_reference(gpu):
     r = p.run(model='nngp', nn=15, seed=45)
     assert r['k'] == int(P['nngp_s45__k'])
     assert r['conv_int'] == list(P['nngp_s45__conv_int'])
-    assert np.max(np.abs(r['u'][:, :, -1] - P['nngp_s45__u'][:, :, -1])) < 1e-8
+    assert np.max(np.abs(r['u'][:, :, -1] - P['nngp_s45__u'][:, :, -1])) < 5e-7   # eps
     assert np.max(np.abs(r['u'][:, :, -1] - P['fine'])) < 1e-5
     assert set(r['timings']) >= {'F_time', 'G_time', 'mdl_tot_t', 'runtime', 'F_time_serial_avg'}
 
