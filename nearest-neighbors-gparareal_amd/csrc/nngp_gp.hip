@@ -280,15 +280,31 @@ __device__ __forceinline__ bool group_factor(int m, int lr, int gbase,
         }
         a[j] = v;
     }
-    // left-looking Cholesky (OpenBLAS potf2 order); jax returns NaN on failure (models.py:89)
+    // left-looking Cholesky; jax returns NaN on failure (models.py:89).  Row j of L reaches the
+    // other lanes by shuffles; sum_k L_rk L_jk is a balanced tree over k (zero padded to a power
+    // of two) -- the same tree as the oracle -- so the dependent chain is log2(j) adds, not j.
     bool fail = false;
     diag_r = 1.0;
+    double rinv_r = 1.0;
 #pragma unroll
     for (int j = 0; j < G; j++) {
         if (j < m) {   // m is wave-uniform: a scalar branch, the loop stays fully unrolled
             double t = a[j];
+            if (j > 0) {
+                double pr[G];
 #pragma unroll
-            for (int k = 0; k < j; k++) t = t - a[k] * __shfl(a[k], gbase + j, 64);
+                for (int k = 0; k < G; k++) pr[k] = (k < j) ? a[k] * __shfl(a[k], gbase + j, 64) : 0.0;
+                int P = 1;
+                while (P < j) P <<= 1;   // compile-time after unrolling
+#pragma unroll
+                for (int sft = 1; sft < G; sft <<= 1)
+                    if (sft < P) {
+#pragma unroll
+                        for (int k = 0; k + sft < G; k += 2 * sft)
+                            if (k < P) pr[k] = pr[k] + pr[k + sft];
+                    }
+                t = t - pr[0];
+            }
             const double piv = __shfl(t, gbase + j, 64);
             fail = fail || !(piv > 0.0);
             const double ljj = sqrt(piv);
@@ -298,15 +314,21 @@ __device__ __forceinline__ bool group_factor(int m, int lr, int gbase,
             } else if (lr == j) {
                 a[j] = ljj;
                 diag_r = ljj;
+                rinv_r = rinv;
             }
         }
     }
+    // division by L_ii as x*r corrected by one fma (Markstein; r = RN(1/L_ii) -> RN(x/L_ii))
+    auto divd = [&](double x) {
+        const double q = x * rinv_r;
+        return fma(fma(-q, diag_r, x), rinv_r, q);
+    };
     // forward solve L z = y (models.py:90, inner solve_triangular)
     double acc = rowv ? y_r : 0.0, z = 0.0;
 #pragma unroll
     for (int i = 0; i < G; i++) {
         if (i < m) {
-            const double zi = __shfl(acc / a[i], gbase + i, 64);
+            const double zi = __shfl(divd(acc), gbase + i, 64);
             if (lr > i) acc = acc - a[i] * zi;
             if (lr == i) z = zi;
         }
@@ -320,7 +342,7 @@ __device__ __forceinline__ bool group_factor(int m, int lr, int gbase,
 #pragma unroll
     for (int i = G - 1; i >= 0; i--) {
         if (i < m) {
-            const double ai = __shfl(acc2 / a[i], gbase + i, 64);
+            const double ai = __shfl(divd(acc2), gbase + i, 64);
             if (lr < i) acc2 = acc2 - Limg[i * G + lr] * ai;
             if (lr == i) alpha = ai;
         }
@@ -714,9 +736,14 @@ static int run_nm(NMArgs &a, bool fused, hipStream_t st) {
     if (fused) {
         const int nfc = a.nj * a.R;
         // whole coordinates per workgroup; keep <= 1024 threads and the LDS under ~150 KB
-        int cpw = (G == 16) ? (36 / nfc) : (18 / nfc);
-        if (cpw < 1) cpw = 1;
-        cpw = std::min(cpw, a.d);
+        // few coordinates per workgroup so the fits spread over every CU (latency-bound NM
+        // chains: one workgroup per CU beats packing), capped by LDS / thread budgets below
+        static int ncu = 0;
+        if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) ncu = 256;
+        if (ncu <= 0) ncu = 256;
+        int cpw = (a.d + ncu - 1) / ncu;
+        const int cpw_max = std::max(1, (G == 16) ? (36 / nfc) : (18 / nfc));
+        cpw = std::max(1, std::min(cpw, std::min(cpw_max, a.d)));
         auto lds_of = [&](int c) {
             const int ng = ((c * nfc * G + 63) / 64) * 64 / G;   // groups incl. padding
             return sizeof(double) * ((size_t)a.m * a.m + a.m + 4 * (size_t)ng + (size_t)ng * G * G);

@@ -452,31 +452,51 @@ static int gp_factor(int m, const double *D2, const double *y, double c, double 
             if (j == r) v = v + jit;
             L[r * m + j] = v;
         }
-    /* left-looking Cholesky (OpenBLAS potf2 order)                                          */
+    /* left-looking Cholesky; sum_k L_ik L_jk as a balanced tree over k (zero padded to the
+     * next power of two) -- the GPU's order                                                   */
+    double rinv_d[64];
     for (int j = 0; j < m; j++) {
+        int P = 1;
+        while (P < j) P <<= 1;
+        double pr[64];
+        /* diagonal */
         double t = L[j * m + j];
-        for (int k = 0; k < j; k++) t = t - L[j * m + k] * L[j * m + k];
+        if (j > 0) {
+            for (int k = 0; k < P; k++) pr[k] = k < j ? L[j * m + k] * L[j * m + k] : 0.0;
+            for (int sft = 1; sft < P; sft <<= 1)
+                for (int k = 0; k + sft < P; k += 2 * sft) pr[k] = pr[k] + pr[k + sft];
+            t = t - pr[0];
+        }
         if (!(t > 0.0)) return 1;           /* ajj <= 0 or NaN: jax -> NaN -> +inf          */
         const double ljj = sqrt(t);
         const double rinv = 1.0 / ljj;
         L[j * m + j] = ljj;
+        rinv_d[j] = rinv;
         for (int i = j + 1; i < m; i++) {
             double s = L[i * m + j];
-            for (int k = 0; k < j; k++) s = s - L[i * m + k] * L[j * m + k];
+            if (j > 0) {
+                for (int k = 0; k < P; k++) pr[k] = k < j ? L[i * m + k] * L[j * m + k] : 0.0;
+                for (int sft = 1; sft < P; sft <<= 1)
+                    for (int k = 0; k + sft < P; k += 2 * sft) pr[k] = pr[k] + pr[k + sft];
+                s = s - pr[0];
+            }
             L[i * m + j] = s * rinv;
         }
     }
-    /* L z = y (forward), L^T alpha = z (backward)                                          */
+    /* L z = y (forward), L^T alpha = z (backward); x / L_ii as the Markstein-corrected
+     * x * RN(1/L_ii), identical to IEEE division (tests/test_oracle_golden.py)              */
     double z[64];
     for (int i = 0; i < m; i++) {
         double s = y[i];
         for (int k = 0; k < i; k++) s = s - L[i * m + k] * z[k];
-        z[i] = s / L[i * m + i];
+        const double q = s * rinv_d[i];
+        z[i] = fma(fma(-q, L[i * m + i], s), rinv_d[i], q);
     }
     for (int i = m - 1; i >= 0; i--) {
         double s = z[i];
         for (int k = m - 1; k > i; k--) s = s - L[k * m + i] * alpha[k];
-        alpha[i] = s / L[i * m + i];
+        const double q = s * rinv_d[i];
+        alpha[i] = fma(fma(-q, L[i * m + i], s), rinv_d[i], q);
     }
     return 0;
 }
