@@ -30,7 +30,7 @@ namespace nngp {
 // ODE right-hand sides (systems.py), one lane = one state
 // ---------------------------------------------------------------------------------------------
 struct LaneArgs {
-    double mn[4], w[4], sc[4];   // '-11' wrapper: mn, (mx-mn), 2/(mx-mn)   (utils.py:14-33)
+    double mn[4], hw[4], sc[4];  // '-11' wrapper: mn, (mx-mn)/2, 2/(mx-mn)   (utils.py:14-33)
     double param[4];
     double rparam0;              // RN(1/param[0]) for the Markstein division below
     int normalized;
@@ -109,20 +109,58 @@ template <> struct LaneSys<NNGP_SYS_DBL_PEND> {  // systems.py:182-189
     }
 };
 
-// f_n(u) = f(inverse(u)) * scale   (systems.py:36-40)
-template <int SYS>
+// f_n(u) = f(inverse(u)) * scale   (systems.py:36-40), inverse(u) = ((u+1)/2)*(mx-mn) + mn
+// (utils.py:24) evaluated as (u+1)*((mx-mn)/2) + mn: halving is exact for normal numbers, so
+// RN(RN(u+1)/2 * w) == RN(RN(u+1) * (w/2)) bit for bit, one multiply fewer per component.  NORM is a template parameter so the RK
+// step loop carries no branches: the lane kernel is VALU-issue-bound (one wave per SIMD, ~4.5
+// cycles per fp64 instruction, dependent or not -- tools/ubench_fp64.hip), so every instruction
+// and every taken scalar branch inside the step is paid in full on the critical path.
+template <int SYS, bool NORM>
 __device__ __forceinline__ void lane_rhs(const double *u, double *o, const LaneArgs &a) {
     constexpr int D = LaneSys<SYS>::D;
-    if (a.normalized) {
+    if constexpr (NORM) {
         double v[D];
 #pragma unroll
-        for (int c = 0; c < D; c++) v[c] = ((u[c] + 1) / 2) * a.w[c] + a.mn[c];
+        for (int c = 0; c < D; c++) v[c] = (u[c] + 1) * a.hw[c] + a.mn[c];
         LaneSys<SYS>::f(v, o, a);
 #pragma unroll
         for (int c = 0; c < D; c++) o[c] = o[c] * a.sc[c];
     } else {
         LaneSys<SYS>::f(u, o, a);
     }
+}
+
+// stage input  u + sum_{j<s} a_sj k_j  over the non-zero a_sj in ascending j (RK.py:153-166).
+// The reference starts the sum from 0.0 (`temp = jnp.zeros(dim)`); starting from the first term
+// instead is identical up to the sign of an exact zero and saves one dependent add per stage.
+// k is indexed k[j*KS + c]; s is a compile-time constant after unrolling.
+template <typename T, int KS>
+__device__ __forceinline__ double stage_input(int s, double u, const double *k, int c) {
+    double t = 0.0;
+    bool first = true;
+#pragma unroll
+    for (int j = 0; j < T::S; j++) {
+        if (j >= s || T::A[s][j] == 0.0) continue;
+        const double v = T::A[s][j] * k[j * KS + c];
+        t = first ? v : t + v;
+        first = false;
+    }
+    return first ? u : u + t;
+}
+
+// u + sum_s b_s k_s over the non-zero b_s in ascending s (jnp.sum(b*k, 1), RK.py:170)
+template <typename T, int KS>
+__device__ __forceinline__ double step_update(double u, const double *k, int c) {
+    double acc = 0.0;
+    bool first = true;
+#pragma unroll
+    for (int s = 0; s < T::S; s++) {
+        if (T::B[s] == 0.0) continue;
+        const double v = T::B[s] * k[s * KS + c];
+        acc = first ? v : acc + v;
+        first = false;
+    }
+    return u + acc;
 }
 
 // FIXED:    h = dt = (t1-t0)/steps (RK.py:103).
@@ -139,7 +177,7 @@ __device__ __forceinline__ double step_size(bool linspace, int64_t n, int64_t j0
     return tn1 - tn;
 }
 
-template <int SYS, int ORDER, bool LINSPACE>
+template <int SYS, int ORDER, bool LINSPACE, bool NORM>
 __global__ void __launch_bounds__(64) rk_lane_kernel(LaneArgs args, int n_slices,
                                                      const double *__restrict__ t0,
                                                      const double *__restrict__ t1, int64_t steps,
@@ -151,15 +189,15 @@ __global__ void __launch_bounds__(64) rk_lane_kernel(LaneArgs args, int n_slices
     constexpr int D = LaneSys<SYS>::D;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_slices) return;
-    if (args.normalized) {
+    if constexpr (NORM) {
 #pragma unroll
         for (int c = 0; c < D; c++) {
             args.mn[c] = args.norm[c];
-            args.w[c] = args.norm[D + c];
+            args.hw[c] = 0.5 * args.norm[D + c];
             args.sc[c] = args.norm[2 * D + c];
         }
     }
-    double u[D], k[S][D], tmp[D];
+    double u[D], k[S * D], tmp[D];
 #pragma unroll
     for (int c = 0; c < D; c++) u[c] = u0[(size_t)i * D + c];
     const double T0 = t0[i], T1 = t1[i];
@@ -167,39 +205,17 @@ __global__ void __launch_bounds__(64) rk_lane_kernel(LaneArgs args, int n_slices
     const int64_t j0 = j0s ? j0s[i] : 0;
     for (int64_t n = 0; n < steps; n++) {
         const double h = step_size(LINSPACE, n, j0, gsteps, T0, T1, dt);
-        // k_0 = h f(u); k_i = h f(u + sum_{j<i} a_ij k_j)     (RK.py:153-170)
+        // k_0 = h f(u); k_s = h f(u + sum_{j<s} a_sj k_j)     (RK.py:153-170)
 #pragma unroll
         for (int s = 0; s < S; s++) {
-            if (s == 0) {
-                lane_rhs<SYS>(u, k[0], args);
-            } else {
 #pragma unroll
-                for (int c = 0; c < D; c++) {
-                    double t = 0.0;
+            for (int c = 0; c < D; c++) tmp[c] = stage_input<T, D>(s, u[c], k, c);
+            lane_rhs<SYS, NORM>(tmp, k + s * D, args);
 #pragma unroll
-                    for (int j = 0; j < s; j++)
-                        if (T::A[s][j] != 0.0) t = t + T::A[s][j] * k[j][c];
-                    tmp[c] = u[c] + t;
-                }
-                lane_rhs<SYS>(tmp, k[s], args);
-            }
-#pragma unroll
-            for (int c = 0; c < D; c++) k[s][c] = h * k[s][c];
+            for (int c = 0; c < D; c++) k[s * D + c] = h * k[s * D + c];
         }
-        // u + jnp.sum(b*k, 1)  (RK.py:170)
 #pragma unroll
-        for (int c = 0; c < D; c++) {
-            double acc = 0.0;
-            bool first = true;
-#pragma unroll
-            for (int s = 0; s < S; s++) {
-                if (T::B[s] == 0.0) continue;
-                const double v = T::B[s] * k[s][c];
-                acc = first ? v : acc + v;
-                first = false;
-            }
-            u[c] = u[c] + acc;
-        }
+        for (int c = 0; c < D; c++) u[c] = step_update<T, D>(u[c], k, c);   // RK.py:170
     }
 #pragma unroll
     for (int c = 0; c < D; c++) uF[(size_t)i * D + c] = u[c];
@@ -276,7 +292,7 @@ __device__ __forceinline__ double fhn_lap(const double *__restrict__ V, const Nb
 }
 
 // <= 256 threads per slice leaves ~170 VGPRs for u, the S stage vectors and the neighbour table
-template <int SYS, int ORDER, bool LINSPACE, int EPT>
+template <int SYS, int ORDER, bool LINSPACE, int EPT, bool NORM>
 __global__ void __launch_bounds__(256) rk_field_kernel(FieldArgs fa, int n_slices,
                                                         const double *__restrict__ t0,
                                                         const double *__restrict__ t1,
@@ -292,7 +308,7 @@ __global__ void __launch_bounds__(256) rk_field_kernel(FieldArgs fa, int n_slice
     const int d = fa.d;
     const int half = d / 2;   // FHN-PDE: u1 | u2
 
-    double u[EPT], k[S][EPT], mn[EPT], w[EPT], sc[EPT];
+    double u[EPT], k[S * EPT], mn[EPT], w[EPT], sc[EPT];
     int e_[EPT];
     Nbr5 nb[(SYS == NNGP_SYS_FHN_PDE) ? EPT : 1];
 #pragma unroll
@@ -301,9 +317,9 @@ __global__ void __launch_bounds__(256) rk_field_kernel(FieldArgs fa, int n_slice
         e_[r] = e;
         const bool ok = e < d;
         u[r] = ok ? u0[(size_t)slice * d + e] : 0.0;
-        if (fa.normalized && ok) {
+        if (NORM && ok) {
             mn[r] = fa.norm[e];
-            w[r] = fa.norm[d + e];
+            w[r] = 0.5 * fa.norm[d + e];   // (mx-mn)/2, see lane_rhs
             sc[r] = fa.norm[2 * d + e];
         } else {
             mn[r] = 0.0; w[r] = 1.0; sc[r] = 1.0;
@@ -322,15 +338,8 @@ __global__ void __launch_bounds__(256) rk_field_kernel(FieldArgs fa, int n_slice
 #pragma unroll
             for (int r = 0; r < EPT; r++) {
                 if (e_[r] < d) {
-                    double x = u[r];
-                    if (s > 0) {
-                        double t = 0.0;
-#pragma unroll
-                        for (int j = 0; j < s; j++)
-                            if (T::A[s][j] != 0.0) t = t + T::A[s][j] * k[j][r];
-                        x = u[r] + t;
-                    }
-                    V[e_[r]] = fa.normalized ? ((x + 1) / 2) * w[r] + mn[r] : x;
+                    const double x = stage_input<T, EPT>(s, u[r], k, r);
+                    V[e_[r]] = NORM ? (x + 1) * w[r] + mn[r] : x;
                 }
             }
             __syncthreads();
@@ -351,25 +360,14 @@ __global__ void __launch_bounds__(256) rk_field_kernel(FieldArgs fa, int n_slice
                             f = (1 / 0.1) * ((lv + V[e - half]) - V[e]);
                         }
                     }
-                    if (fa.normalized) f = f * sc[r];
+                    if (NORM) f = f * sc[r];
                 }
-                k[s][r] = h * f;
+                k[s * EPT + r] = h * f;
             }
             buf ^= 1;
         }
 #pragma unroll
-        for (int r = 0; r < EPT; r++) {
-            double acc = 0.0;
-            bool first = true;
-#pragma unroll
-            for (int s = 0; s < S; s++) {
-                if (T::B[s] == 0.0) continue;
-                const double v = T::B[s] * k[s][r];
-                acc = first ? v : acc + v;
-                first = false;
-            }
-            u[r] = u[r] + acc;
-        }
+        for (int r = 0; r < EPT; r++) u[r] = step_update<T, EPT>(u[r], k, r);   // RK.py:170
     }
 #pragma unroll
     for (int r = 0; r < EPT; r++)
@@ -388,12 +386,15 @@ __global__ void __launch_bounds__(64) rhs_lane_kernel(LaneArgs args, int n, cons
     if (args.normalized)
         for (int c = 0; c < D; c++) {
             args.mn[c] = args.norm[c];
-            args.w[c] = args.norm[D + c];
+            args.hw[c] = 0.5 * args.norm[D + c];
             args.sc[c] = args.norm[2 * D + c];
         }
     double x[D], o[D];
     for (int c = 0; c < D; c++) x[c] = u[(size_t)i * D + c];
-    lane_rhs<SYS>(x, o, args);
+    if (args.normalized)
+        lane_rhs<SYS, true>(x, o, args);
+    else
+        lane_rhs<SYS, false>(x, o, args);
     for (int c = 0; c < D; c++) out[(size_t)i * D + c] = o[c];
 }
 
@@ -450,8 +451,12 @@ static int launch_lane(const nngp_system *sys, int n, const double *t0, const do
     a.norm = sys->norm;
     NNGP_REQUIRE(!sys->normalized || sys->norm != nullptr, "normalized system needs norm[3d]");
     const int bs = 64;
-    hipLaunchKernelGGL((rk_lane_kernel<SYS, ORDER, LIN>), dim3((n + bs - 1) / bs), dim3(bs), 0, st,
-                       a, n, t0, t1, steps, gsteps, j0, u0, uF);
+    if (sys->normalized)
+        hipLaunchKernelGGL((rk_lane_kernel<SYS, ORDER, LIN, true>), dim3((n + bs - 1) / bs), dim3(bs), 0, st,
+                           a, n, t0, t1, steps, gsteps, j0, u0, uF);
+    else
+        hipLaunchKernelGGL((rk_lane_kernel<SYS, ORDER, LIN, false>), dim3((n + bs - 1) / bs), dim3(bs), 0,
+                           st, a, n, t0, t1, steps, gsteps, j0, u0, uF);
     NNGP_LAUNCH_CHECK();
     return NNGP_OK;
 }
@@ -461,8 +466,12 @@ static int launch_field_ept(const FieldArgs &fa, int bt, int n, const double *t0
                             const double *t1, int64_t steps, int64_t gsteps, const int64_t *j0,
                             const double *u0, double *uF, hipStream_t st) {
     const size_t lds = sizeof(double) * 2 * (size_t)fa.d;
-    hipLaunchKernelGGL((rk_field_kernel<SYS, ORDER, LIN, EPT>), dim3(n), dim3(bt), lds, st, fa, n,
-                       t0, t1, steps, gsteps, j0, u0, uF);
+    if (fa.normalized)
+        hipLaunchKernelGGL((rk_field_kernel<SYS, ORDER, LIN, EPT, true>), dim3(n), dim3(bt), lds, st, fa, n,
+                           t0, t1, steps, gsteps, j0, u0, uF);
+    else
+        hipLaunchKernelGGL((rk_field_kernel<SYS, ORDER, LIN, EPT, false>), dim3(n), dim3(bt), lds, st, fa, n,
+                           t0, t1, steps, gsteps, j0, u0, uF);
     NNGP_LAUNCH_CHECK();
     return NNGP_OK;
 }

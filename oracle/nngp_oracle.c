@@ -281,11 +281,18 @@ int orc_rk_grid(const nngp_system *sys, int order, int mode, double t0, double t
         orc_rhs(sys, u, k, scr);
         for (int c = 0; c < d; c++) k[c] = h * k[c];
         for (int i = 1; i < S; i++) {
+            /* the reference sums from temp = 0 (RK.py:153-166); starting from the first non-zero
+             * term is identical up to the sign of an exact zero (the HIP kernels do the same)    */
             for (int c = 0; c < d; c++) {
                 double t = 0.0;
-                for (int j = 0; j < i; j++)
-                    if (T.a[i][j] != 0.0) t = t + T.a[i][j] * k[(size_t)j * d + c];
-                tmp[c] = u[c] + t;
+                int first = 1;
+                for (int j = 0; j < i; j++) {
+                    if (T.a[i][j] == 0.0) continue;
+                    const double v = T.a[i][j] * k[(size_t)j * d + c];
+                    t = first ? v : t + v;
+                    first = 0;
+                }
+                tmp[c] = first ? u[c] : u[c] + t;
             }
             double *ki = k + (size_t)i * d;
             orc_rhs(sys, tmp, ki, scr);
