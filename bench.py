@@ -29,6 +29,13 @@ sys.path.insert(0, ROOT)
 
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector: half the 157.3 TF FP32 vector peak (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
+# One-wave issue floor of the lane kernel: a slice is one dependent chain, so a
+# step costs (fp64 VALU per step) x (cycles per wave64 fp64 VALU issue).  119 VALU per Hopf RK4
+# step in the gfx950 code object (tools/isa_loop_count.py); 4.22 cycles per independent
+# v_mul/v_add_f64 and a 2.40 GHz shader clock measured on the box (tools/ubench_fp64.hip).
+LANE_VALU_PER_STEP = 119
+CYCLES_PER_F64_VALU = 4.22
+SHADER_GHZ = 2.40
 # algorithmic flops per fine step per slice: S*F_rhs + (2 nnz(a) + S + 2 nnz(b))*d
 FLOPS_PER_STEP = {('hopf', 'RK4'): 126, ('hopf', 'RK8'): 11 * 18 + (2 * 39 + 11 + 2 * 5) * 3,
                   ('burgers', 'RK8'): 28160}
@@ -204,6 +211,10 @@ def main():
         'roofline': {'bound': 'fp64-valu', 'achieved': achieved_tf, 'peak': FP64_PEAK_TFLOPS,
                      'unit': 'TFLOP/s', 'frac': achieved_tf / FP64_PEAK_TFLOPS, 'traffic': read_traffic(),
                      'kernel': 'rk_lane_kernel<HOPF,RK4>', 'kernel_ms': kernel_s * 1e3,
+                     'issue_floor_us_per_step': LANE_VALU_PER_STEP * CYCLES_PER_F64_VALU / (SHADER_GHZ * 1e3),
+                     'us_per_step': kernel_s / args.steps_per_slice * 1e6,
+                     'issue_floor_frac': (LANE_VALU_PER_STEP * CYCLES_PER_F64_VALU / (SHADER_GHZ * 1e9))
+                                         / (kernel_s / args.steps_per_slice),
                      'flops_per_step_per_slice': FLOPS_PER_STEP[('hopf', 'RK4')]},
     }
     if rank == 0 and world == 1 and not args.no_extras:

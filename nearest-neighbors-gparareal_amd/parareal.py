@@ -69,6 +69,45 @@ class _Events:
         return out
 
 
+def shard_bounds(I, N, world, rank):
+    """Contiguous block of the unconverged slices [I, N) owned by `rank`: every
+    rank gets ceil((N-I)/world) slices (the last ones fewer or none), so one fixed-size all-gather
+    reassembles them in slice order.  Returns (lo, hi, chunk)."""
+    n_c = N - I
+    chunk = (n_c + world - 1) // world
+    lo = I + min(rank * chunk, n_c)
+    hi = I + min((rank + 1) * chunk, n_c)
+    return lo, hi, chunk
+
+
+def fine_sweep_sharded(propagate, t, U, UF, I, N, group=None):
+    """The fine sweep of one Parareal iteration, UF[I+1:N+1] = F(t[I:N], t[I+1:N+1], U[I:N])
+    (parareal.py:310-327), sharded over the ranks of `group`: each rank integrates its contiguous
+    block with ONE batched launch (`propagate(t0, t1, U0, out)`), then a single all-gather of the
+    [chunk][d] end states (RCCL over xGMI; gloo on CPU) gives every rank the full result.  That
+    all-gather is the only collective of the Parareal iteration."""
+    import torch
+    dist = torch.distributed
+    world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+    if world == 1:
+        propagate(t[I:N], t[I + 1:N + 1], U[I:N], UF[I + 1:N + 1])
+        return
+    rank = dist.get_rank(group)
+    lo, hi, chunk = shard_bounds(I, N, world, rank)
+    n = U.shape[1]
+    send = torch.zeros((chunk, n), dtype=U.dtype, device=U.device)
+    if hi > lo:
+        propagate(t[lo:hi], t[lo + 1:hi + 1], U[lo:hi].contiguous(), send[:hi - lo])
+    if dist.get_backend(group) == 'gloo':
+        parts = [torch.empty_like(send) for _ in range(world)]
+        dist.all_gather(parts, send, group=group)
+        gathered = torch.cat(parts)
+    else:
+        gathered = torch.empty((world * chunk, n), dtype=U.dtype, device=U.device)
+        dist.all_gather_into_tensor(gathered, send, group=group)
+    UF[I + 1:N + 1] = gathered[:N - I]
+
+
 class Parareal():
 
     def __init__(self, ode, solver, tspan, N, epsilon=5e-7, verbose='v', process_group=None, **kwargs):
@@ -132,25 +171,8 @@ class Parareal():
     # ------------------------------------------------------------------------------ F sweep
     def _fine_sweep(self, torch, t_dev, Uk, UF, I, N, n):
         """uF[I+1:N+1] = F(u[I:N]) -- sharded over ranks when a process group is active."""
-        pg = self.process_group
-        world = 1
-        if pg is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
-            world = torch.distributed.get_world_size(pg)
-        if world == 1:
-            self.solver.run_F_batch(t_dev[I:N], t_dev[I + 1:N + 1], Uk[I:N], out=UF[I + 1:N + 1])
-            return
-        rank = torch.distributed.get_rank(pg)
-        n_c = N - I
-        chunk = (n_c + world - 1) // world
-        lo = I + min(rank * chunk, n_c)
-        hi = I + min((rank + 1) * chunk, n_c)
-        send = torch.zeros((chunk, n), dtype=torch.float64, device=Uk.device)
-        if hi > lo:
-            self.solver.run_F_batch(t_dev[lo:hi], t_dev[lo + 1:hi + 1], Uk[lo:hi].contiguous(),
-                                    out=send[:hi - lo])
-        gathered = torch.empty((world * chunk, n), dtype=torch.float64, device=Uk.device)
-        torch.distributed.all_gather_into_tensor(gathered, send, group=pg)
-        UF[I + 1:N + 1] = gathered[:n_c]
+        fine_sweep_sharded(lambda a, b, u, out: self.solver.run_F_batch(a, b, u, out=out),
+                           t_dev, Uk, UF, I, N, self.process_group)
 
     # --------------------------------------------------------------------------- main loop
     def _parareal(self, model, debug=False, early_stop=None, parall='Serial', store_int=False,
