@@ -259,134 +259,265 @@ __global__ void __launch_bounds__(256) d2_kernel(const double *__restrict__ xm, 
 }
 
 // ---------------------------------------------------------------------------------------------
-// group-level GP factorisation: K = psy*exp(c*D2) + jit*I, Cholesky, L z = y, L^T alpha = z
-// lane r (0 <= r < G) of the group owns row r; lanes r >= m carry zeros.
+// GP likelihood of one fit on ONE 16-lane DPP row
+//
+// A fit owns one row of a wave (lanes 16g .. 16g+15).  Lane l holds rows l and, for m > 16
+// (RPL = 2), l+16 of the m x m kernel matrix in VGPRs.  Every cross-lane move of the
+// factorisation is a broadcast of one lane to its row -- `v_mov_b64_dpp row_newbcast:L` on
+// gfx950, one VALU op, no LDS round trip -- and the two reductions are 4-level DPP butterflies.
+// The wave is VALU-issue-bound (tools/ubench_fp64.hip), so the design goal is the smallest
+// instruction count per likelihood evaluation:
+//   * K's lower triangle (m(m+1)/2 exps) is spread evenly over the 16 lanes (lane l builds
+//     entries l, l+16, ... of the flattened triangle, with their D2 values preloaded once per fit)
+//     and redistributed to the row owners through a small LDS image;
+//   * left-looking Cholesky with row broadcasts; forward solve with broadcasts; back solve from
+//     the transposed L read back from the same LDS image.
+// Arithmetic order (restated in oracle/nngp_oracle.c gp_factor / butterfly_sum):
+//   K_rj = psy*exp(c*D2_rj) (+ jit on the diagonal)                 models.py:146-155, 88
+//   L_ij = (((K_ij - L_i0 L_j0) - L_i1 L_j1) - ...) * RN(1/L_jj)      potrf, k ascending
+//   z, alpha: successive subtraction, k ascending / descending; x/L_ii as Markstein x*RN(1/L_ii)
+//   sums over rows: lane pairs (l, l+16) first, then butterfly levels 1, 2, 4, 8
 // ---------------------------------------------------------------------------------------------
-template <int G>
-__device__ __forceinline__ bool group_factor(int m, int lr, int gbase,
-                                             const double *__restrict__ sD2, double c, double psy,
-                                             double jit, double y_r, double *Limg, double &alpha_r,
-                                             double &diag_r) {
-    double a[G];
-    const bool rowv = lr < m;
-    const double *drow = sD2 + (rowv ? lr : 0) * m;
-#pragma unroll
-    for (int j = 0; j < G; j++) {
-        double v = 0.0;
-        if (j < m) {   // wave-uniform
-            const double e = psy * nn_exp(c * drow[j]);     // k_gauss, models.py:146-148
-            v = (rowv && j <= lr) ? e : 0.0;
-            v = (rowv && j == lr) ? v + jit : v;             // + eye*10**jitter, models.py:88
-        }
-        a[j] = v;
-    }
-    // left-looking Cholesky; jax returns NaN on failure (models.py:89).  Row j of L reaches the
-    // other lanes by shuffles; sum_k L_rk L_jk is a balanced tree over k (zero padded to a power
-    // of two) -- the same tree as the oracle -- so the dependent chain is log2(j) adds, not j.
-    bool fail = false;
-    diag_r = 1.0;
-    double rinv_r = 1.0;
-#pragma unroll
-    for (int j = 0; j < G; j++) {
-        if (j < m) {   // m is wave-uniform: a scalar branch, the loop stays fully unrolled
-            double t = a[j];
-            if (j > 0) {
-                double pr[G];
-#pragma unroll
-                for (int k = 0; k < G; k++) pr[k] = (k < j) ? a[k] * __shfl(a[k], gbase + j, 64) : 0.0;
-                int P = 1;
-                while (P < j) P <<= 1;   // compile-time after unrolling
-#pragma unroll
-                for (int sft = 1; sft < G; sft <<= 1)
-                    if (sft < P) {
-#pragma unroll
-                        for (int k = 0; k + sft < G; k += 2 * sft)
-                            if (k < P) pr[k] = pr[k] + pr[k + sft];
-                    }
-                t = t - pr[0];
-            }
-            const double piv = __shfl(t, gbase + j, 64);
-            fail = fail || !(piv > 0.0);
-            const double ljj = sqrt(piv);
-            const double rinv = 1.0 / ljj;
-            if (lr > j) {
-                a[j] = t * rinv;
-            } else if (lr == j) {
-                a[j] = ljj;
-                diag_r = ljj;
-                rinv_r = rinv;
-            }
-        }
-    }
-    // division by L_ii as x*r corrected by one fma (Markstein; r = RN(1/L_ii) -> RN(x/L_ii))
-    auto divd = [&](double x) {
-        const double q = x * rinv_r;
-        return fma(fma(-q, diag_r, x), rinv_r, q);
-    };
-    // forward solve L z = y (models.py:90, inner solve_triangular)
-    double acc = rowv ? y_r : 0.0, z = 0.0;
-#pragma unroll
-    for (int i = 0; i < G; i++) {
-        if (i < m) {
-            const double zi = __shfl(divd(acc), gbase + i, 64);
-            if (lr > i) acc = acc - a[i] * zi;
-            if (lr == i) z = zi;
-        }
-    }
-    // rows of L to the group's LDS image for the transposed (back) solve
-#pragma unroll
-    for (int k = 0; k < G; k++)
-        if (k < m && rowv && k <= lr) Limg[lr * G + k] = a[k];
-    wave_lds_sync();
-    double acc2 = z, alpha = 0.0;
-#pragma unroll
-    for (int i = G - 1; i >= 0; i--) {
-        if (i < m) {
-            const double ai = __shfl(divd(acc2), gbase + i, 64);
-            if (lr < i) acc2 = acc2 - Limg[i * G + lr] * ai;
-            if (lr == i) alpha = ai;
-        }
-    }
-    wave_lds_sync();
-    alpha_r = alpha;
-    return !fail;
+template <int L>
+__device__ __forceinline__ double row_bcast(double v) {   // every lane <- lane L of its 16-row
+    return __builtin_amdgcn_mov_dpp(v, 0x150 + L, 0xF, 0xF, false);
 }
 
-template <int G>
-__device__ __forceinline__ double group_sum(double v) {
-#pragma unroll
-    for (int s = 1; s < G; s <<= 1) v = v + __shfl_xor(v, s, 64);
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+
+// sum over the 16 lanes of a row, xor-butterfly order: quad_perm [1,0,3,2], quad_perm [2,3,0,1],
+// row_half_mirror, row_mirror.  After level s every lane of an aligned 2s-block holds the same
+// partial sum, so the mirrors deliver exactly the xor partner's value; a+b == b+a keeps every
+// lane bit-identical.
+__device__ __forceinline__ double row_sum(double v) {
+    v = v + dpp_mov<0xB1>(v);
+    v = v + dpp_mov<0x4E>(v);
+    v = v + dpp_mov<0x141>(v);
+    v = v + dpp_mov<0x140>(v);
     return v;
 }
 
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+// A fit of size m runs padded to MAXM (one of 8, 16, 24, 32): rows m..MAXM-1 are identity rows
+// of K with y = 0.  The padded factorisation is exact -- L = [[L_m, 0], [0, I]], z and alpha
+// pad with exact zeros, every real row's arithmetic is untouched -- so every loop has a
+// compile-time trip count and no per-j branches.
+template <int MAXM_> struct GP {
+    static constexpr int MAXM = MAXM_;
+    static constexpr int RPL = MAXM > 16 ? 2 : 1;                      // rows per lane
+    static constexpr int S = MAXM + 1;                                  // LDS row stride (pad)
+    static constexpr int IMG = 16 * RPL * S;                            // image doubles / fit
+    static constexpr int NQ = (MAXM * (MAXM + 1) / 2 + 15) / 16;       // triangle entries / lane
+};
+
+// per-lane, theta-independent part of a fit: where its share of the triangle lives
+// (idxq[q] = diagonal << 30 | D2 index << 16 | K-image slot; D2 index < 2^10, slot < 2^16)
+template <int MAXM> struct GPLane {
+    int idxq[GP<MAXM>::NQ];
+    int nq;           // entries this lane builds (<= NQ)
+};
+
+template <int MAXM>
+__device__ __forceinline__ void gp_lane_init(GPLane<MAXM> &P, int m, int l) {
+    constexpr int S = GP<MAXM>::S;
+    const int T = m * (m + 1) / 2;
+    P.nq = 0;
+    int r = 0;
+#pragma unroll
+    for (int q = 0; q < GP<MAXM>::NQ; q++) {
+        const int t = l + 16 * q;
+        P.idxq[q] = 0;
+        if (t < T) {
+            while ((r + 1) * (r + 2) / 2 <= t) r++;
+            const int j = t - r * (r + 1) / 2;
+            P.idxq[q] = ((j == r) << 30) | ((r * m + j) << 16) | (r * S + j);
+            P.nq = q + 1;
+        }
+    }
+}
+
+// The fit's LDS image: rows >= m (the pad) are identity rows, written once per kernel and never
+// overwritten (the triangle build and the L write-back touch rows < m only).
+template <int MAXM>
+__device__ __forceinline__ void gp_image_init(double *Kimg, int m, int l) {
+    constexpr int RPL = GP<MAXM>::RPL, S = GP<MAXM>::S;
+#pragma unroll
+    for (int s = 0; s < RPL; s++) {
+        const int row = l + 16 * s;
+#pragma unroll
+        for (int j = 0; j < MAXM; j++) Kimg[row * S + j] = (row >= m && j == row) ? 1.0 : 0.0;
+    }
+    wave_lds_sync();
+}
+
+// Factor K = psy*exp(c*D2) + jit*I and solve; returns false if potrf fails (jax: NaN).
+// alpha[s], diag[s] are those of row l + 16 s (meaningful for rows < m).
+template <int MAXM>
+__device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, const double *sD2,
+                                          double c, double psy, double jit,
+                                          const double (&y)[GP<MAXM>::RPL], double *Kimg,
+                                          double (&alpha)[GP<MAXM>::RPL],
+                                          double (&diag)[GP<MAXM>::RPL]) {
+    constexpr int RPL = GP<MAXM>::RPL, S = GP<MAXM>::S, NQ = GP<MAXM>::NQ;
+    // 1) this lane's share of the triangle -> LDS image K[r*S + j]
+    wave_lds_sync();
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+        if (q < P.nq) {
+            const int ix = P.idxq[q];
+            double e = psy * nn_exp(c * sD2[(ix >> 16) & 0x3FF]);    // k_gauss, models.py:146-148
+            if (ix >> 30) e = e + jit;                                // + eye*10**jitter, :88
+            Kimg[ix & 0xFFFF] = e;
+        }
+    }
+    wave_lds_sync();
+    // 2) own rows into registers (pad rows are the image's identity rows; the upper triangle
+    //    is never used)
+    double a[RPL][MAXM];
+#pragma unroll
+    for (int s = 0; s < RPL; s++)
+#pragma unroll
+        for (int j = 0; j < MAXM; j++)
+            if (j < 16 * (s + 1)) a[s][j] = Kimg[(l + 16 * s) * S + j];
+    // 3) left-looking Cholesky, row j broadcast from lane j%16 of set j/16.  The pivot is
+    //    broadcast, so every lane computes L_jj and RN(1/L_jj) identically; the row owner keeps
+    //    them.  Updates of rows < j (upper triangle) are computed and ignored: fewer
+    //    instructions than masking them.
+    bool fail = false;
+    double rinv[RPL];
+#pragma unroll
+    for (int s = 0; s < RPL; s++) {
+        diag[s] = 1.0;
+        rinv[s] = 1.0;
+    }
+    static_for<0, MAXM>([&](auto jc) {
+        constexpr int j = decltype(jc)::value, SJ = j / 16, LJ = j % 16;
+        double t[RPL];
+#pragma unroll
+        for (int s = 0; s < RPL; s++)
+            if (16 * (s + 1) > j) t[s] = a[s][j];
+#pragma unroll
+        for (int k = 0; k < j; k++) {
+            const double ljk = row_bcast<LJ>(a[SJ][k]);
+#pragma unroll
+            for (int s = 0; s < RPL; s++)
+                if (16 * (s + 1) > j) t[s] = t[s] - a[s][k] * ljk;
+        }
+        const double piv = row_bcast<LJ>(t[SJ]);
+        fail = fail || !(piv > 0.0);
+        const double ljj = sqrt(piv);
+        const double ri = 1.0 / ljj;
+        diag[SJ] = (l == LJ) ? ljj : diag[SJ];
+        rinv[SJ] = (l == LJ) ? ri : rinv[SJ];
+#pragma unroll
+        for (int s = 0; s < RPL; s++)
+            if (16 * (s + 1) > j) a[s][j] = (l + 16 * s == j) ? ljj : t[s] * ri;
+    });
+    // x / L_ii for this lane's row of set s: Markstein-corrected x * RN(1/L_ii) (= IEEE x/L_ii)
+    auto divd = [&](int s, double x) {
+        const double q = x * rinv[s];
+        return fma(fma(-q, diag[s], x), rinv[s], q);
+    };
+    // 4) forward solve L z = y (models.py:90, inner solve_triangular); rows <= i update
+    //    harmlessly (their z is already captured)
+    double acc[RPL], z[RPL];
+#pragma unroll
+    for (int s = 0; s < RPL; s++) {
+        acc[s] = y[s];
+        z[s] = 0.0;
+    }
+    static_for<0, MAXM>([&](auto ic) {
+        constexpr int i = decltype(ic)::value, SI = i / 16, LI = i % 16;
+        const double zi = row_bcast<LI>(divd(SI, acc[SI]));
+        z[SI] = (l == LI) ? zi : z[SI];
+#pragma unroll
+        for (int s = 0; s < RPL; s++)
+            if (16 * (s + 1) > i + 1) acc[s] = acc[s] - a[s][i] * zi;
+    });
+    // 5) back solve L^T alpha = z: L to the LDS image, column of this lane's row(s) back
+    wave_lds_sync();
+#pragma unroll
+    for (int s = 0; s < RPL; s++) {
+        if (l + 16 * s < m) {   // real rows only: the pad rows of the image stay identity
+#pragma unroll
+            for (int j = 0; j < MAXM; j++)
+                if (j < 16 * (s + 1)) Kimg[(l + 16 * s) * S + j] = a[s][j];
+        }
+    }
+    wave_lds_sync();
+    double acc2[RPL];
+#pragma unroll
+    for (int s = 0; s < RPL; s++) {
+        acc2[s] = z[s];
+        alpha[s] = 0.0;
+    }
+    static_for<0, MAXM>([&](auto ic) {
+        constexpr int i = MAXM - 1 - decltype(ic)::value, SI = i / 16, LI = i % 16;
+        const double ai = row_bcast<LI>(divd(SI, acc2[SI]));
+        alpha[SI] = (l == LI) ? ai : alpha[SI];
+#pragma unroll
+        for (int s = 0; s < RPL; s++)
+            if (16 * s < i) acc2[s] = acc2[s] - Kimg[i * S + l + 16 * s] * ai;   // L[i][row]
+    });
+    return !fail;
+}
+
+// sum over the fit's rows r < m of v[r] (pairs (l, l+16) first -- oracle butterfly_sum)
+template <int RPL>
+__device__ __forceinline__ double gp_rows_sum(int m, int l, const double (&v)[RPL]) {
+    double p = (l < m) ? v[0] : 0.0;
+    if constexpr (RPL == 2) p = p + ((l + 16 < m) ? v[1] : 0.0);
+    return row_sum(p);
+}
+
 // -LML (models.py:240-252): NaN (incl. failed Cholesky) -> +inf
-template <int G>
-__device__ __forceinline__ double group_nlml(int m, int lr, int gbase, const double *sD2,
-                                             double sx, double sy, double jit, double y_r,
-                                             double *Limg) {
+template <int MAXM>
+__device__ __forceinline__ double gp_nlml(int m, int l, const GPLane<MAXM> &P, const double *sD2,
+                                          double sx, double sy,
+                                          double jit, const double (&y)[GP<MAXM>::RPL], double *Kimg) {
+    constexpr int RPL = GP<MAXM>::RPL;
     const double c = -0.5 * (1 / nn_pow10(sx));
     const double psy = nn_pow10(sy);
-    double alpha, diag;
-    const bool ok = group_factor<G>(m, lr, gbase, sD2, c, psy, jit, y_r, Limg, alpha, diag);
-    const bool rowv = lr < m;
-    const double ydot = group_sum<G>(rowv ? y_r * alpha : 0.0);
-    const double slog = group_sum<G>(rowv ? nn_log(diag) : 0.0);
+    double alpha[RPL], diag[RPL], ya[RPL], lg[RPL];
+    const bool ok = gp_factor<MAXM>(m, l, P, sD2, c, psy, jit, y, Kimg, alpha, diag);
+#pragma unroll
+    for (int s = 0; s < RPL; s++) {
+        ya[s] = y[s] * alpha[s];
+        lg[s] = nn_log(diag[s]);
+    }
+    const double ydot = gp_rows_sum<RPL>(m, l, ya);
+    const double slog = gp_rows_sum<RPL>(m, l, lg);
     const double res = -(((-0.5 * ydot) - slog) - ((double)m / 2) * LOG_2PI);
     return (!ok || res != res) ? INFINITY : res;
 }
 
 // posterior mean K(xm, new_x)^T alpha (models.py:162-168); NaN on Cholesky failure
-template <int G>
-__device__ __forceinline__ double group_mean(int m, int lr, int gbase, const double *sD2,
-                                             const double *skd2, double sx, double sy, double jit,
-                                             double y_r, double *Limg) {
+template <int MAXM>
+__device__ __forceinline__ double gp_mean(int m, int l, const GPLane<MAXM> &P, const double *sD2,
+                                          const double *skd2,
+                                          double sx, double sy, double jit,
+                                          const double (&y)[GP<MAXM>::RPL], double *Kimg) {
+    constexpr int RPL = GP<MAXM>::RPL;
     const double c = -0.5 * (1 / nn_pow10(sx));
     const double psy = nn_pow10(sy);
-    double alpha, diag;
-    const bool ok = group_factor<G>(m, lr, gbase, sD2, c, psy, jit, y_r, Limg, alpha, diag);
-    const bool rowv = lr < m;
-    const double ks = rowv ? psy * nn_exp(c * skd2[lr]) : 0.0;
-    const double mean = group_sum<G>(rowv ? ks * alpha : 0.0);
+    double alpha[RPL], diag[RPL], ka[RPL];
+    const bool ok = gp_factor<MAXM>(m, l, P, sD2, c, psy, jit, y, Kimg, alpha, diag);
+#pragma unroll
+    for (int s = 0; s < RPL; s++) {
+        const int row = l + 16 * s;
+        ka[s] = (psy * nn_exp(c * skd2[row < m ? row : 0])) * alpha[s];
+    }
+    const double mean = gp_rows_sum<RPL>(m, l, ka);
     return ok ? mean : NAN;
 }
 
@@ -571,26 +702,24 @@ __device__ __forceinline__ double jit_lookup(const NMArgs &a, int j) {
     return v;
 }
 
-// register budget: G=16 needs ~162 VGPRs (3 waves/SIMD -> <= 768 threads), G=32 ~245
-// (2 waves/SIMD -> <= 512 threads); tighter bounds make the compiler spill to scratch
-template <int G> struct NMBound { static constexpr int T = (G == 16) ? 768 : 512; };
+// register budget: MAXM <= 16 fits 256 VGPRs (<= 512 threads), MAXM <= 32 needs up to 512 (256)
+template <int MAXM> struct NMBound { static constexpr int T = (MAXM <= 16) ? 512 : 256; };
 
-template <int G, bool FUSED>
-__global__ void __launch_bounds__(NMBound<G>::T) nm_fit_kernel(NMArgs a) {
+template <int MAXM, bool FUSED>
+__global__ void __launch_bounds__(NMBound<MAXM>::T) nm_fit_kernel(NMArgs a) {
+    constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG;
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int m = a.m;
     const int nfc = a.nj * a.R;                         // fits per coordinate
-    const int ngroups = FUSED ? a.cpw * nfc : (int)(blockDim.x / G);
-    const int galloc = blockDim.x / G;                  // groups incl. padding lanes
+    const int galloc = blockDim.x / 16;                 // groups incl. padding lanes
+    const int ngroups = FUSED ? a.cpw * nfc : galloc;
     double *sD2 = sm;
     double *skd2 = sD2 + m * m;
     double *sRes = skd2 + m;                            // [galloc][4]
-    double *sL = sRes + galloc * 4;                     // [galloc][G*G]
+    double *sK = sRes + galloc * 4;                     // [galloc][IMG]
     const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int g = tid / G;                              // group in block
-    const int lr = tid % G;
-    const int gbase = (lane / G) * G;
+    const int g = tid / 16;                             // group (= DPP row) in block
+    const int l = tid % 16;
 
     for (int i = tid; i < m * m; i += blockDim.x) sD2[i] = a.D2[i];
     if (FUSED)
@@ -609,58 +738,71 @@ __global__ void __launch_bounds__(NMBound<G>::T) nm_fit_kernel(NMArgs a) {
         } else {
             f = blockIdx.x * ngroups + g;
             valid = f < a.n_fits;
-            if (valid) {
+            if (valid && a.coord) {
                 coord = a.coord[f];
                 jidx = a.jitter_idx[f];
+            } else if (valid) {   // product(coord, jitter, restart) order (models.py:186)
+                coord = f / nfc;
+                jidx = (f % nfc) / a.R;
             }
         }
     }
-    const double y_r = (valid && lr < m) ? a.Y[(int64_t)coord * a.ys_c + (int64_t)lr * a.ys_r] : 0.0;
+    double y[RPL];
+#pragma unroll
+    for (int s = 0; s < RPL; s++) {
+        const int row = l + 16 * s;
+        y[s] = (valid && row < m) ? a.Y[(int64_t)coord * a.ys_c + (int64_t)row * a.ys_r] : 0.0;
+    }
     const double jit = valid ? jit_lookup(a, jidx) : 1.0;
-    double *Limg = sL + (size_t)g * G * G;
+    double *Kimg = sK + (size_t)g * IMG;
+    GPLane<MAXM> P;
+    gp_lane_init<MAXM>(P, m, l);
+    gp_image_init<MAXM>(Kimg, m, l);
 
     NMCfg cfg{a.fatol, a.xatol, a.maxfev, a.maxfev};
-    NM S;
-    S.fcalls = 0;
-    S.iters = 0;
-    S.f0 = S.f1 = S.f2 = INFINITY;
-    S.xbx = S.xby = S.xrx = S.xry = S.fxr = 0.0;
+    NM St;
+    St.fcalls = 0;
+    St.iters = 0;
+    St.f0 = St.f1 = St.f2 = INFINITY;
+    St.xbx = St.xby = St.xrx = St.xry = St.fxr = 0.0;
     if (valid) {
         const double t0x = a.theta0[2 * f], t0y = a.theta0[2 * f + 1];
-        S.s0x = t0x; S.s0y = t0y;
-        S.s1x = (t0x != 0) ? (1 + 0.05) * t0x : 0.00025; S.s1y = t0y;   // nonzdelt / zdelt
-        S.s2x = t0x; S.s2y = (t0y != 0) ? (1 + 0.05) * t0y : 0.00025;
-        S.st = ST_INIT0;
-        if (!nm_req(S, cfg, S.s0x, S.s0y, ST_INIT0)) S.st = ST_DONE;
+        St.s0x = t0x; St.s0y = t0y;
+        St.s1x = (t0x != 0) ? (1 + 0.05) * t0x : 0.00025; St.s1y = t0y;   // nonzdelt / zdelt
+        St.s2x = t0x; St.s2y = (t0y != 0) ? (1 + 0.05) * t0y : 0.00025;
+        St.st = ST_INIT0;
+        if (!nm_req(St, cfg, St.s0x, St.s0y, ST_INIT0)) St.st = ST_DONE;
     } else {
-        S.s0x = S.s0y = S.s1x = S.s1y = S.s2x = S.s2y = 0.0;
-        S.px = S.py = 0.0;
-        S.st = ST_DONE;
+        St.s0x = St.s0y = St.s1x = St.s1y = St.s2x = St.s2y = 0.0;
+        St.px = St.py = 0.0;
+        St.st = ST_DONE;
     }
+    // every group of the wave evaluates once per trip until the wave's last fit is done, so the
+    // evaluation code never diverges (finished groups evaluate a dummy point)
     while (true) {
-        const bool need = S.st != ST_DONE;
+        const bool need = St.st != ST_DONE;
         if (!__any(need)) break;
-        const double fv = group_nlml<G>(m, lr, gbase, sD2, S.px, S.py, jit, y_r, Limg);
-        if (need) nm_consume(S, cfg, fv);
+        const double fv = gp_nlml<MAXM>(m, l, P, sD2, St.px, St.py, jit, y, Kimg);
+        if (need) nm_consume(St, cfg, fv);
     }
-    const double fval = (S.f1 != S.f1 || S.f2 != S.f2) ? NAN : S.f0;
-    if (valid && lr == 0) {
-        if (a.theta_out) { a.theta_out[2 * f] = S.s0x; a.theta_out[2 * f + 1] = S.s0y; }
+    const double fval = (St.f1 != St.f1 || St.f2 != St.f2) ? NAN : St.f0;
+    if (valid && l == 0) {
+        if (a.theta_out) { a.theta_out[2 * f] = St.s0x; a.theta_out[2 * f + 1] = St.s0y; }
         if (a.fval_out) a.fval_out[f] = fval;
-        if (a.nfev_out) a.nfev_out[f] = S.fcalls;
+        if (a.nfev_out) a.nfev_out[f] = St.fcalls;
         if (a.fits_out) {
-            a.fits_out[4 * f + 0] = S.s0x;
-            a.fits_out[4 * f + 1] = S.s0y;
+            a.fits_out[4 * f + 0] = St.s0x;
+            a.fits_out[4 * f + 1] = St.s0y;
             a.fits_out[4 * f + 2] = fval;
-            a.fits_out[4 * f + 3] = (double)S.fcalls;
+            a.fits_out[4 * f + 3] = (double)St.fcalls;
         }
         if (FUSED) {
-            sRes[4 * g + 0] = S.s0x;
-            sRes[4 * g + 1] = S.s0y;
+            sRes[4 * g + 0] = St.s0x;
+            sRes[4 * g + 1] = St.s0y;
             sRes[4 * g + 2] = fval;
         }
     }
-    if (!FUSED) return;
+    if constexpr (!FUSED) return;
     __syncthreads();
     // first group of each coordinate: first arg-min over its nfc fits (models.py:207-215 reduces
     // to a first-occurrence arg-min), then the posterior mean with that (theta, jitter)
@@ -676,35 +818,66 @@ __global__ void __launch_bounds__(NMBound<G>::T) nm_fit_kernel(NMArgs a) {
         }
         const double sx = sRes[4 * (g + best)], sy = sRes[4 * (g + best) + 1];
         const double jb = jit_lookup(a, best / a.R);
-        const double mean = group_mean<G>(m, lr, gbase, sD2, skd2, sx, sy, jb, y_r, Limg);
-        if (lr == 0) {
+        const double mean = gp_mean<MAXM>(m, l, P, sD2, skd2, sx, sy, jb, y, Kimg);
+        if (l == 0) {
             a.preds[coord] = mean;
             if (a.out) a.out[coord] = a.bias ? mean + a.bias[coord] : mean;
         }
     }
 }
 
-// posterior mean for given (theta, jitter) per coordinate; one group per coordinate
-template <int G>
-__global__ void __launch_bounds__(256) gp_mean_kernel(int m, int d, const double *__restrict__ D2,
-                                                      const double *__restrict__ kd2,
-                                                      const double *__restrict__ ym,
-                                                      const double *__restrict__ theta,
-                                                      const int32_t *__restrict__ jitter_idx,
-                                                      NMArgs jt, double *__restrict__ out) {
+// posterior mean per coordinate, one 16-lane group per coordinate (models.py:162-168, 217).
+// (theta, jitter) either given (a.theta0[c], a.jitter_idx[c]: nngp_gp_mean) or the first arg-min
+// of the coordinate's a.nj*a.R fits in a.fits_out (the unfused nngp_predict path, used when a
+// coordinate's fits do not fit one workgroup).  Writes a.preds[c] and a.out[c] = mean (+ bias).
+template <int MAXM>
+__global__ void __launch_bounds__(256) gp_mean_kernel(NMArgs a) {
+    constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG;
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    double *sD2 = sm, *skd2 = sm + m * m, *sL = skd2 + m;
-    const int tid = threadIdx.x, lane = tid & 63, g = tid / G, lr = tid % G, gbase = (lane / G) * G;
-    for (int i = tid; i < m * m; i += blockDim.x) sD2[i] = D2[i];
-    for (int i = tid; i < m; i += blockDim.x) skd2[i] = kd2[i];
+    const int m = a.m, d = a.d;
+    double *sD2 = sm, *skd2 = sm + m * m, *sK = skd2 + m;
+    const int tid = threadIdx.x, g = tid / 16, l = tid % 16;
+    for (int i = tid; i < m * m; i += blockDim.x) sD2[i] = a.D2[i];
+    for (int i = tid; i < m; i += blockDim.x) skd2[i] = a.kd2[i];
     __syncthreads();
-    const int c = blockIdx.x * (blockDim.x / G) + g;
+    const int c = blockIdx.x * (blockDim.x / 16) + g;
     const bool valid = c < d;
     const int cc = valid ? c : 0;
-    const double y_r = (valid && lr < m) ? ym[(int64_t)lr * d + cc] : 0.0;
-    const double mean = group_mean<G>(m, lr, gbase, sD2, skd2, theta[2 * cc], theta[2 * cc + 1],
-                                      jit_lookup(jt, jitter_idx[cc]), y_r, sL + (size_t)g * G * G);
-    if (valid && lr == 0) out[c] = mean;
+    double y[RPL];
+#pragma unroll
+    for (int s = 0; s < RPL; s++) {
+        const int row = l + 16 * s;
+        y[s] = (valid && row < m) ? a.Y[(int64_t)cc * a.ys_c + (int64_t)row * a.ys_r] : 0.0;
+    }
+    double sx, sy;
+    int jidx;
+    if (a.fits_out) {
+        const int nfc = a.nj * a.R;
+        const double *F = a.fits_out + (size_t)4 * cc * nfc;
+        int best = 0;
+        double bv = F[2];
+        for (int t = 1; t < nfc; t++)
+            if (F[4 * t + 2] < bv) {
+                bv = F[4 * t + 2];
+                best = t;
+            }
+        sx = F[4 * best];
+        sy = F[4 * best + 1];
+        jidx = best / a.R;
+    } else {
+        sx = a.theta0[2 * cc];
+        sy = a.theta0[2 * cc + 1];
+        jidx = a.jitter_idx[cc];
+    }
+    GPLane<MAXM> P;
+    gp_lane_init<MAXM>(P, m, l);
+    double *Kimg = sK + (size_t)g * IMG;
+    gp_image_init<MAXM>(Kimg, m, l);
+    const double mean = gp_mean<MAXM>(m, l, P, sD2, skd2, sx, sy, jit_lookup(a, jidx), y, Kimg);
+    if (valid && l == 0) {
+        if (a.preds) a.preds[c] = mean;
+        if (a.out) a.out[c] = a.bias ? mean + a.bias[c] : mean;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -718,59 +891,73 @@ static int fill_jitters(NMArgs &a, int n_jitter, const double *jexp) {
     return NNGP_OK;
 }
 
-static int group_size_for(int m) { return m <= 16 ? 16 : 32; }
+// padded fit size: the kernel instantiations (8, 16, 24, 32)
+static int maxm_for(int m) { return m <= 8 ? 8 : (m <= 16 ? 16 : (m <= 24 ? 24 : 32)); }
+static size_t k_image_doubles(int maxm) { return (size_t)16 * (maxm > 16 ? 2 : 1) * (maxm + 1); }
 
-template <int G>
+template <int MAXM>
 static int launch_nm(NMArgs &a, bool fused, int nblocks, int threads, size_t lds, hipStream_t st) {
     if (fused)
-        hipLaunchKernelGGL((nm_fit_kernel<G, true>), dim3(nblocks), dim3(threads), lds, st, a);
+        hipLaunchKernelGGL((nm_fit_kernel<MAXM, true>), dim3(nblocks), dim3(threads), lds, st, a);
     else
-        hipLaunchKernelGGL((nm_fit_kernel<G, false>), dim3(nblocks), dim3(threads), lds, st, a);
+        hipLaunchKernelGGL((nm_fit_kernel<MAXM, false>), dim3(nblocks), dim3(threads), lds, st, a);
+    NNGP_LAUNCH_CHECK();
+    return NNGP_OK;
+}
+
+static int run_mean(NMArgs &a, hipStream_t st) {
+    const int maxm = maxm_for(a.m);
+    const int threads = 256, per = threads / 16;
+    const size_t lds = sizeof(double) * ((size_t)a.m * a.m + a.m + (size_t)per * k_image_doubles(maxm));
+    const dim3 grid((a.d + per - 1) / per);
+    switch (maxm) {
+    case 8: hipLaunchKernelGGL(gp_mean_kernel<8>, grid, dim3(threads), lds, st, a); break;
+    case 16: hipLaunchKernelGGL(gp_mean_kernel<16>, grid, dim3(threads), lds, st, a); break;
+    case 24: hipLaunchKernelGGL(gp_mean_kernel<24>, grid, dim3(threads), lds, st, a); break;
+    default: hipLaunchKernelGGL(gp_mean_kernel<32>, grid, dim3(threads), lds, st, a); break;
+    }
     NNGP_LAUNCH_CHECK();
     return NNGP_OK;
 }
 
 static int run_nm(NMArgs &a, bool fused, hipStream_t st) {
-    const int G = group_size_for(a.m);
-    int threads, nblocks, ngroups;
+    const int maxm = maxm_for(a.m);
+    const size_t kimg = k_image_doubles(maxm);
+    const int tmax = maxm <= 16 ? NMBound<16>::T : NMBound<32>::T;
+    auto lds_of = [&](int threads) {
+        const int galloc = threads / 16;
+        return sizeof(double) * ((size_t)a.m * a.m + a.m + 4 * (size_t)galloc + (size_t)galloc * kimg);
+    };
+    int threads, nblocks;
     if (fused) {
+        // whole coordinates per workgroup (the arg-min needs all fits of a coordinate); few per
+        // workgroup so the latency-bound fits spread over every CU, capped by LDS / threads
         const int nfc = a.nj * a.R;
-        // whole coordinates per workgroup; keep <= 1024 threads and the LDS under ~150 KB
-        // few coordinates per workgroup so the fits spread over every CU (latency-bound NM
-        // chains: one workgroup per CU beats packing), capped by LDS / thread budgets below
         static int ncu = 0;
         if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) ncu = 256;
         if (ncu <= 0) ncu = 256;
-        int cpw = (a.d + ncu - 1) / ncu;
-        const int cpw_max = std::max(1, (G == 16) ? (36 / nfc) : (18 / nfc));
-        cpw = std::max(1, std::min(cpw, std::min(cpw_max, a.d)));
-        auto lds_of = [&](int c) {
-            const int ng = ((c * nfc * G + 63) / 64) * 64 / G;   // groups incl. padding
-            return sizeof(double) * ((size_t)a.m * a.m + a.m + 4 * (size_t)ng + (size_t)ng * G * G);
-        };
-        const int tmax = (G == 16) ? NMBound<16>::T : NMBound<32>::T;
-        auto thr = [&](int c) { return ((c * nfc * G + 63) / 64) * 64; };
-        while (cpw > 1 && (lds_of(cpw) > 150 * 1024 || thr(cpw) > tmax)) cpw--;
-        if (lds_of(cpw) > 150 * 1024 || thr(cpw) > tmax) {
+        auto thr = [&](int c) { return ((c * nfc * 16 + 63) / 64) * 64; };
+        int cpw = std::max(1, std::min((a.d + ncu - 1) / ncu, a.d));
+        while (cpw > 1 && (lds_of(thr(cpw)) > 150 * 1024 || thr(cpw) > tmax)) cpw--;
+        if (lds_of(thr(cpw)) > 150 * 1024 || thr(cpw) > tmax) {
             set_error("m=%d with %d fits per coordinate exceeds the fused kernel's LDS/threads", a.m, nfc);
             return NNGP_E_UNSUPPORTED;
         }
         a.cpw = cpw;
-        ngroups = cpw * nfc;
-        (void)ngroups;
-        threads = ((ngroups * G + 63) / 64) * 64;
+        threads = thr(cpw);
         nblocks = (a.d + cpw - 1) / cpw;
     } else {
         threads = 256;
-        ngroups = threads / G;
-        (void)ngroups;
-        nblocks = (a.n_fits + ngroups - 1) / ngroups;
+        nblocks = (a.n_fits + threads / 16 - 1) / (threads / 16);
         a.cpw = 1;
     }
-    const int galloc = threads / G;
-    const size_t lds = sizeof(double) * ((size_t)a.m * a.m + a.m + 4 * (size_t)galloc + (size_t)galloc * G * G);
-    if (G == 16) return launch_nm<16>(a, fused, nblocks, threads, lds, st);
-    return launch_nm<32>(a, fused, nblocks, threads, lds, st);
+    const size_t lds = lds_of(threads);
+    switch (maxm) {
+    case 8: return launch_nm<8>(a, fused, nblocks, threads, lds, st);
+    case 16: return launch_nm<16>(a, fused, nblocks, threads, lds, st);
+    case 24: return launch_nm<24>(a, fused, nblocks, threads, lds, st);
+    default: return launch_nm<32>(a, fused, nblocks, threads, lds, st);
+    }
 }
 
 }  // namespace nngp
@@ -839,17 +1026,12 @@ extern "C" int nngp_gp_mean(int m, int d, const double *xm, const double *ym, co
     double *kd2 = D2 + m * m;
     hipLaunchKernelGGL(d2_kernel, dim3(1), dim3(256), 0, st, xm, m, d, new_x, D2, kd2);
     NNGP_LAUNCH_CHECK();
-    const int G = group_size_for(m);
-    const int threads = 256, per = threads / G;
-    const size_t lds = sizeof(double) * ((size_t)m * m + m + (size_t)per * G * G);
-    if (G == 16)
-        hipLaunchKernelGGL(gp_mean_kernel<16>, dim3((d + per - 1) / per), dim3(threads), lds, st, m, d, D2,
-                           kd2, ym, theta, jitter_idx, jt, out);
-    else
-        hipLaunchKernelGGL(gp_mean_kernel<32>, dim3((d + per - 1) / per), dim3(threads), lds, st, m, d, D2,
-                           kd2, ym, theta, jitter_idx, jt, out);
-    NNGP_LAUNCH_CHECK();
-    return NNGP_OK;
+    NMArgs ma{};
+    rc = fill_jitters(ma, n_jitter, jitter_exp_host);
+    if (rc) return rc;
+    ma.m = m; ma.d = d; ma.D2 = D2; ma.kd2 = kd2; ma.Y = ym; ma.ys_c = 1; ma.ys_r = d;
+    ma.theta0 = theta; ma.jitter_idx = jitter_idx; ma.R = 1; ma.preds = out;
+    return run_mean(ma, st);
 }
 
 extern "C" int nngp_predict(const double *X, const double *Y, int64_t rows, int d, const double *new_x,
@@ -865,10 +1047,12 @@ extern "C" int nngp_predict(const double *X, const double *Y, int64_t rows, int 
     NMArgs a{};
     int rc = fill_jitters(a, n_jitter, jitter_exp_host);
     if (rc) return rc;
-    // workspace: dist[rows] | D2[m*m] | kd2[m] | ymT[d*m] | idx[m] (int32)
+    // workspace: dist[rows] | D2[m*m] | kd2[m] | ymT[d*m] | idx[m] (int32) | fits[n_fits][4]
+    // (the fits scratch serves the unfused fallback below when the caller passes no fits_out)
     const size_t nd = (size_t)rows + (size_t)m * m + m + (size_t)d * m;
+    const size_t n_fits = (size_t)d * n_jitter * n_restarts;
     int err = 0;
-    char *ws = (char *)workspace(sizeof(double) * nd + sizeof(int32_t) * 64, &err);
+    char *ws = (char *)workspace(sizeof(double) * nd + sizeof(int32_t) * 64 + sizeof(double) * 4 * n_fits, &err);
     if (err) return err;
     double *dist = (double *)ws;
     double *D2 = dist + rows;
@@ -885,5 +1069,14 @@ extern "C" int nngp_predict(const double *X, const double *Y, int64_t rows, int 
     a.D2 = D2; a.kd2 = kd2; a.Y = ymT; a.ys_c = m; a.ys_r = 1;
     a.theta0 = theta0; a.fatol = fatol; a.xatol = xatol; a.maxfev = maxfev; a.R = n_restarts;
     a.fits_out = fits_out; a.preds = preds_out; a.bias = bias; a.out = out;
-    return run_nm(a, true, st);
+    rc = run_nm(a, true, st);
+    if (rc != NNGP_E_UNSUPPORTED) return rc;
+    // a coordinate's fits exceed one workgroup (large m with restarts): fits kernel, then the
+    // per-coordinate arg-min + posterior mean kernel
+    if (!fits_out) a.fits_out = (double *)(ws + sizeof(double) * nd + sizeof(int32_t) * 64);
+    NMArgs u = a;
+    u.preds = nullptr; u.out = nullptr; u.bias = nullptr;
+    rc = run_nm(u, false, st);
+    if (rc) return rc;
+    return run_mean(a, st);
 }

@@ -437,19 +437,30 @@ double orc_sqdist_pairwise(const double *a, const double *b, int d, double *scra
     return pairwise_sum(scratch, d);
 }
 
-static int group_size(int m) { return m <= 16 ? 16 : (m <= 32 ? 32 : 64); }
-
-/* xor-butterfly over G lanes (zero padded), as the GPU reduces: level s adds lanes r, r^s,
- * so lane 0 pairs (0,1),(2,3),... first, then (0,2),... -- a balanced tree.                */
-static double butterfly_sum(const double *v, int n, int G) {
-    double buf[64];
-    for (int i = 0; i < G; i++) buf[i] = i < n ? v[i] : 0.0;
-    for (int s = 1; s < G; s <<= 1)
-        for (int i = 0; i < G; i += 2 * s) buf[i] = buf[i] + buf[i + s];
+/* Cross-lane sum of the GPU's 16-lane group (one DPP row): lane l holds rows l and, for
+ * m > 16, l+16, which it adds first; then xor-butterfly levels 1, 2, 4, 8 -- lane 0 pairs
+ * (0,1),(2,3),... first, then (0,2),... -- a balanced tree.  Rows >= n contribute 0.0.       */
+static double butterfly_sum(const double *v, int n) {
+    double buf[16];
+    for (int i = 0; i < 16; i++) {
+        buf[i] = i < n ? v[i] : 0.0;
+        if (n > 16) buf[i] = buf[i] + (i + 16 < n ? v[i + 16] : 0.0);
+    }
+    for (int s = 1; s < 16; s <<= 1)
+        for (int i = 0; i < 16; i += 2 * s) buf[i] = buf[i] + buf[i + s];
     return buf[0];
 }
 
-/* Cholesky + solves for K = psy*exp(c*D2) + jit*I.  Returns 0 ok, 1 if potrf fails.        */
+/* Cholesky + solves for K = psy*exp(c*D2) + jit*I.  Returns 0 ok, 1 if potrf fails.
+ * The reference's order belongs to LAPACK/OpenBLAS potrf + trsv inside jaxlib, so ONE order is
+ * fixed here and in the HIP kernel: left-looking, row-oriented, every inner product a
+ * sequential ascending sum of rounded products subtracted one at a time
+ *     L_ij = (((K_ij - L_i0 L_j0) - L_i1 L_j1) - ...) * RN(1/L_jj),
+ * forward z_i (k ascending), back alpha_i (k descending), each division the Markstein-
+ * corrected x*RN(1/L_ii) (bitwise the IEEE quotient).  Of the orders tried against the
+ * reference's own LML fixtures (tests/golden/lml.npz), this one agrees best on WHICH
+ * near-singular kernels fail potrf (99.8 % of the duplicated-row grid, vs 99 % for a balanced
+ * tree and 96 % for an FMA chain) -- the pass/fail bit that steers Nelder-Mead.               */
 static int gp_factor(int m, const double *D2, const double *y, double c, double psy, double jit,
                      double *L /*m*m*/, double *alpha) {
     /* build lower triangle (models.py:146-155, 88) */
@@ -459,21 +470,10 @@ static int gp_factor(int m, const double *D2, const double *y, double c, double 
             if (j == r) v = v + jit;
             L[r * m + j] = v;
         }
-    /* left-looking Cholesky; sum_k L_ik L_jk as a balanced tree over k (zero padded to the
-     * next power of two) -- the GPU's order                                                   */
     double rinv_d[64];
     for (int j = 0; j < m; j++) {
-        int P = 1;
-        while (P < j) P <<= 1;
-        double pr[64];
-        /* diagonal */
         double t = L[j * m + j];
-        if (j > 0) {
-            for (int k = 0; k < P; k++) pr[k] = k < j ? L[j * m + k] * L[j * m + k] : 0.0;
-            for (int sft = 1; sft < P; sft <<= 1)
-                for (int k = 0; k + sft < P; k += 2 * sft) pr[k] = pr[k] + pr[k + sft];
-            t = t - pr[0];
-        }
+        for (int k = 0; k < j; k++) t = t - L[j * m + k] * L[j * m + k];
         if (!(t > 0.0)) return 1;           /* ajj <= 0 or NaN: jax -> NaN -> +inf          */
         const double ljj = sqrt(t);
         const double rinv = 1.0 / ljj;
@@ -481,17 +481,10 @@ static int gp_factor(int m, const double *D2, const double *y, double c, double 
         rinv_d[j] = rinv;
         for (int i = j + 1; i < m; i++) {
             double s = L[i * m + j];
-            if (j > 0) {
-                for (int k = 0; k < P; k++) pr[k] = k < j ? L[i * m + k] * L[j * m + k] : 0.0;
-                for (int sft = 1; sft < P; sft <<= 1)
-                    for (int k = 0; k + sft < P; k += 2 * sft) pr[k] = pr[k] + pr[k + sft];
-                s = s - pr[0];
-            }
+            for (int k = 0; k < j; k++) s = s - L[i * m + k] * L[j * m + k];
             L[i * m + j] = s * rinv;
         }
     }
-    /* L z = y (forward), L^T alpha = z (backward); x / L_ii as the Markstein-corrected
-     * x * RN(1/L_ii), identical to IEEE division (tests/test_oracle_golden.py)              */
     double z[64];
     for (int i = 0; i < m; i++) {
         double s = y[i];
@@ -515,12 +508,11 @@ double orc_nlml(int m, const double *D2, const double *y, double sx, double sy, 
     double L[64 * 64], alpha[64], tmp[64];
     const double c = -0.5 * (1 / nn_pow10(sx));
     const double psy = nn_pow10(sy);
-    const int G = group_size(m);
     if (gp_factor(m, D2, y, c, psy, jit, L, alpha)) return INFINITY;
     for (int i = 0; i < m; i++) tmp[i] = y[i] * alpha[i];
-    const double ydot = butterfly_sum(tmp, m, G);
+    const double ydot = butterfly_sum(tmp, m);
     for (int i = 0; i < m; i++) tmp[i] = nn_log(L[i * m + i]);
-    const double slog = butterfly_sum(tmp, m, G);
+    const double slog = butterfly_sum(tmp, m);
     const double res = -(((-0.5 * ydot) - slog) - ((double)m / 2) * LOG_2PI);
     if (isnan(res)) return INFINITY;
     return res;
@@ -534,7 +526,7 @@ double orc_gp_mean_one(int m, const double *D2, const double *kd2, const double 
     const double psy = nn_pow10(sy);
     if (gp_factor(m, D2, y, c, psy, jit, L, alpha)) return NAN;
     for (int i = 0; i < m; i++) tmp[i] = (psy * nn_exp(c * kd2[i])) * alpha[i];
-    return butterfly_sum(tmp, m, group_size(m));
+    return butterfly_sum(tmp, m);
 }
 
 /* numpy's small-array argsort is insertion sort (stable); NaN sort last                      */
@@ -730,7 +722,7 @@ void orc_knn(const double *X, int64_t rows, int d, const double *q, int m, int32
 int orc_predict(const double *X, const double *Y, int64_t rows, int d, const double *q, int m,
                 int nj, const double *jit_exp, int R, const double *theta0, double fatol,
                 double xatol, int maxfev, double *preds, double *fits_out, int nthreads) {
-    if (m < 1 || m > 64 || m > rows) return -1;
+    if (m < 1 || m > 32 || m > rows) return -1;
     int32_t *idx = (int32_t *)malloc(sizeof(int32_t) * m);
     double *xm = (double *)malloc(sizeof(double) * m * d);
     double *ymT = (double *)malloc(sizeof(double) * m * d); /* [d][m] */

@@ -177,7 +177,7 @@ def test_gp_mean_vs_oracle(gpu):
     got = mdl.gp_mean(L['xm'], L['ym'], L['new_x'], th, np.array([5, 5, 5], dtype=np.int32))
     for j in range(3):
         ora = O.gp_mean(L['xm'], L['ym'][:, j], L['new_x'], th[j], -15.0)
-        assert abs(got[j] - ora) <= 1e-13 * max(1e-3, abs(ora))
+        assert got[j] == ora                                   # same operation order: bitwise
         ref = L['post_mean_jit15'][40 + j, j]
         assert abs(got[j] - ref) <= 1e-8
 
@@ -226,3 +226,25 @@ def test_predict_restarts_and_small_training_set(gpu):
     th0 = np.random.default_rng(5).integers(-8, 0, (3 * 9 * 2, 2)).astype(float)
     ora = O.predict(xm, ym, xm[0] + 0.01, 8, th0, n_restarts=2)
     assert np.max(np.abs(got - ora)) <= 1e-12 * max(1e-6, np.max(np.abs(ora)))
+
+
+@pytest.mark.parametrize('m,d,R', [(5, 3, 1), (12, 4, 2), (16, 3, 2), (20, 6, 1), (20, 3, 2), (30, 2, 2)])
+def test_predict_every_padded_size_and_fallback_vs_oracle(gpu, m, d, R):
+    """Fits run padded to 8/16/24/32 rows (identity pad, exact); m > 16 with 2 restarts exceeds
+    one workgroup per coordinate and takes the unfused fits + arg-min/mean path.  Bitwise."""
+    import torch
+    rng = np.random.default_rng(m * 10 + d + R)
+    X = np.cumsum(0.05 * rng.standard_normal((3 * m, d)), axis=0)
+    Y = 0.01 * np.sin(3 * X) + 1e-5 * rng.standard_normal(X.shape)
+    q = X[m] + 0.01
+    mdl = gpu.NNGP_p(n=d, N=4, nn=m, n_restarts=R, seed=3)
+    th0 = mdl.draw_thetas(1)
+    fits = torch.empty((mdl.n_fits, 4), dtype=torch.float64, device='cuda')
+    bias = rng.standard_normal(d)
+    out = torch.empty(d, dtype=torch.float64, device='cuda')
+    preds = mdl.predict_device(_t(torch, X), _t(torch, Y), X.shape[0], _t(torch, q), _t(torch, th0),
+                               fits_out=fits, out=out, bias=_t(torch, bias)).cpu().numpy()
+    ora, ofits = O.predict(X, Y, q, m, th0, n_restarts=R, return_fits=True)
+    assert np.array_equal(fits.cpu().numpy(), ofits)
+    assert np.array_equal(preds, ora)
+    assert np.array_equal(out.cpu().numpy(), ora + bias)
