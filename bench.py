@@ -169,6 +169,33 @@ def cpu_baseline(steps_per_slice_full, n_slices, target_s=10.0):
                       f'{dt:.1f} s, oracle/nngp_oracle.c -O2 OpenMP'}
 
 
+def burgers_iter1(torch, g):
+    """GPU: the first nnGParareal iteration (fine sweep + 127 sequential corrections) of the
+    Burgers N=128 config, wall-clock (the CPU leg below times the same iteration)."""
+    ode = g.Burgers(d_x=128, normalization='-11')
+    solver = g.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
+    p = g.Parareal(ode, solver, [0, 5], 128, epsilon=5e-7, verbose=None)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r = p.run(model='nngp', nn=15, seed=45, early_stop=1)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, r
+
+
+def burgers_cpu_iter1(threads):
+    """CPU baseline for the north star's Burgers target: the oracle's C restatement (OpenMP over
+    slices for F and over the 1 152 fits of each correction) runs the same first iteration."""
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import oracle as O
+    s = O.System('burgers', d=128, param=(0.01,), mn=0.0, mx=1.0)
+    x = np.linspace(-1, 1, 128)
+    u0 = s.fit(0.5 * (np.cos(4.5 * np.pi * x) + 1))
+    t0 = time.perf_counter()
+    r = O.parareal(s, [0, 5], 128, 4, 2000, 'RK1', 'RK8', model='nngp', nn=15, seed=45, u0=u0,
+                   nthreads=threads, early_stop=1)
+    return time.perf_counter() - t0, r
+
+
 def read_traffic():
     path = os.path.join(ROOT, 'profiles', 'fine_kernel_traffic.json')
     if os.path.exists(path):
@@ -227,6 +254,18 @@ def main():
                                                    'F_time_s': tim['F_time'], 'mdl_time_s': tim['mdl_tot_t']}
             log(which, 'converged', conv, 'K', k, f'{wall:.2f}s')
         res['cpu_baseline'] = cpu_baseline(args.steps_per_slice, args.slices_per_gpu)
+        # north-star target (>= 10x the CPU path on Burgers N=128, identical K): time the first
+        # iteration on both sides and extrapolate the CPU to the GPU run's K
+        g_s, g_r = burgers_iter1(torch, g)
+        c_s, c_r = burgers_cpu_iter1(res['cpu_baseline']['cores'])
+        same = bool(np.array_equal(np.nan_to_num(g_r['u'], nan=7.0), np.nan_to_num(c_r['u'], nan=7.0)))
+        conv = res['burgers_n128_to_convergence']
+        res['burgers_n128_vs_cpu'] = {
+            'gpu_iter1_s': g_s, 'cpu_iter1_s': c_s, 'iter1_speedup': c_s / g_s,
+            'iter1_bitwise_equal': same, 'cpu_cores': res['cpu_baseline']['cores'],
+            'cpu_to_convergence_est_s': c_s / g_s * conv['wall_s'],
+            'note': 'CPU = oracle C restatement (OpenMP), first Parareal iteration of the same run; '
+                    'full-run CPU time extrapolated by the iteration-1 ratio'}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
