@@ -160,6 +160,26 @@ int nngp_predict(const double *X, const double *Y, int64_t rows, int d, const do
                  double *preds_out, const double *bias, double *out, double *fits_out,
                  void *stream);
 
+/* ---- 3. the sequential correction sweep of one Parareal iteration ------------------------
+ * Replaces the loop parareal.py:359-382 (legacy new_lib.py:990-1012): for i = I .. N-1
+ *     UG1[i+1] = G(t[i], t[i+1], U1[i])                     run_G_timed, parareal.py:361
+ *     U1[i+1]  = correction(U1[i]) + UG1[i+1]                  parareal.py:367-368, 382
+ * with correction = (UF[i+1] - UG[i+1]) for NNGP_MODEL_PARAREAL (models.py:82-83) or the
+ * nnGP prediction for NNGP_MODEL_NNGP (= nngp_predict on X/Y[rows][d] with m neighbours,
+ * theta0 = the (N-I) predictions' initial thetas back to back, [(N-I)][d*n_jitter*n_restarts][2]).
+ * All slice launches are queued on `stream` without host synchronisation.
+ *   t: DEVICE [N+1]; U1, UG1: DEVICE [N+1][d] (rows I.. read, rows I+1.. written);
+ *   UF, UG: DEVICE [N+1][d] (parareal model only); preds_scratch: DEVICE [d] (nngp only);
+ *   g_ms_out: HOST, total device time of the G launches (ms), or NULL (no timing events).    */
+#define NNGP_MODEL_PARAREAL 0
+#define NNGP_MODEL_NNGP 1
+int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps,
+                          const double *t, int I, int N, double *U1, double *UG1, const double *UF,
+                          const double *UG, int model, const double *X, const double *Y, int64_t rows,
+                          int m, int n_jitter, const double *jitter_exp_host, int n_restarts,
+                          const double *theta0, double fatol, double xatol, int maxfev,
+                          double *preds_scratch, float *g_ms_out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

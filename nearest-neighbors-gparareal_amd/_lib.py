@@ -22,7 +22,8 @@ STEP_FIXED, STEP_LINSPACE = 0, 1
 
 EXPORTS = ['nngp_abi_version', 'nngp_last_error', 'nngp_device_count', 'nngp_rk_batch', 'nngp_rk_batch_grid',
            'nngp_rhs_batch', 'nngp_parareal_update', 'nngp_knn', 'nngp_nm_fit_batch',
-           'nngp_gp_mean', 'nngp_predict']
+           'nngp_gp_mean', 'nngp_predict', 'nngp_correction_sweep']
+MODEL_PARAREAL, MODEL_NNGP = 0, 1
 
 
 class NNGPError(RuntimeError):
@@ -70,6 +71,9 @@ def lib():
     L.nngp_gp_mean.argtypes = [i32, i32, _vp, _vp, _vp, _vp, _vp, i32, _dp, _vp, _vp]
     L.nngp_predict.argtypes = [_vp, _vp, i64, i32, _vp, i32, i32, _dp, i32, _vp, dbl, dbl, i32, _vp,
                                _vp, _vp, _vp, _vp]
+    L.nngp_correction_sweep.argtypes = [ctypes.POINTER(CSystem), i32, i32, i64, _vp, i32, i32, _vp, _vp, _vp,
+                                        _vp, i32, _vp, _vp, i64, i32, i32, _dp, i32, _vp, dbl, dbl, i32,
+                                        _vp, ctypes.POINTER(ctypes.c_float), _vp]
     for name in EXPORTS:
         if name not in ('nngp_abi_version', 'nngp_last_error', 'nngp_device_count'):
             getattr(L, name).restype = i32

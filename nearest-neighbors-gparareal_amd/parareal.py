@@ -23,7 +23,7 @@ import warnings
 import numpy as np
 
 from . import _lib
-from .models import BareParareal, NNGP_p
+from .models import JITTERS, BareParareal, NNGP_p
 from .solver import SolverAbstr
 from .systems import ODE
 
@@ -174,6 +174,55 @@ class Parareal():
         fine_sweep_sharded(lambda a, b, u, out: self.solver.run_F_batch(a, b, u, out=out),
                            t_dev, Uk, UF, I, N, self.process_group)
 
+    # ------------------------------------------------------------------ correction sweep
+    def _correction_sweep(self, torch, model, t_dev, I, N, U1, UG1, UF, UG, X, Y, rows, th0, stream):
+        """The sequential sweep i = I..N-1 of parareal.py:359-382 (G, correction, u = preds + uG)
+        as ONE native call (nngp_correction_sweep) that queues every slice's launches back to back.
+        Returns the device time of the G launches in seconds."""
+        solver, lib = self.solver, _lib.lib()
+        if N <= I:
+            return 0.0
+        if solver.Ng > solver.thresh:   # paged coarse solve (never in the reference configs)
+            return self._correction_sweep_py(torch, model, t_dev, I, N, U1, UG1, UF, UG, X, Y, rows,
+                                             th0, stream)
+        cs = solver.f.csystem(U1.device)
+        g_ms = ctypes.c_float(0.0)
+        if isinstance(model, NNGP_p):
+            m = min(model.n_neighbours(), int(rows))
+            jit, jp = _lib.host_doubles(JITTERS)
+            if not hasattr(self, '_preds_scratch') or self._preds_scratch.device != U1.device:
+                self._preds_scratch = torch.empty(self.n, dtype=torch.float64, device=U1.device)
+            _lib.check(lib.nngp_correction_sweep(
+                ctypes.byref(cs), _lib.TABLEAU[solver.G], solver.step_mode, solver.Ng, t_dev.data_ptr(), I, N,
+                U1.data_ptr(), UG1.data_ptr(), None, None, _lib.MODEL_NNGP, X.data_ptr(), Y.data_ptr(),
+                int(rows), m, len(jit), jp, model.n_restarts, th0.data_ptr(), float(model.fatol),
+                float(model.xatol), model.maxfev, self._preds_scratch.data_ptr(), ctypes.byref(g_ms), stream))
+            model.train_count += model.n_fits * (N - I)
+        else:
+            _lib.check(lib.nngp_correction_sweep(
+                ctypes.byref(cs), _lib.TABLEAU[solver.G], solver.step_mode, solver.Ng, t_dev.data_ptr(), I, N,
+                U1.data_ptr(), UG1.data_ptr(), UF.data_ptr(), UG.data_ptr(), _lib.MODEL_PARAREAL, None, None,
+                0, 0, 0, None, 0, None, 0.0, 0.0, 0, None, ctypes.byref(g_ms), stream))
+        return g_ms.value / 1e3
+
+    def _correction_sweep_py(self, torch, model, t_dev, I, N, U1, UG1, UF, UG, X, Y, rows, th0, stream):
+        """Per-slice Python loop (paged coarse solver only): same launches, issued one by one."""
+        lib = _lib.lib()
+        ev = _Events(torch)
+        nf = model.n_fits if isinstance(model, NNGP_p) else 0
+        for i in range(I, N):
+            eg = ev.start()
+            self.solver.run_G_batch(t_dev[i:i + 1], t_dev[i + 1:i + 2], U1[i:i + 1], out=UG1[i + 1:i + 2])
+            ev.stop(eg, 'G')
+            if isinstance(model, NNGP_p):
+                j = i - I
+                model.predict_device(X, Y, rows, U1[i], th0[j * nf:(j + 1) * nf], out=U1[i + 1],
+                                     bias=UG1[i + 1], stream=stream)
+            else:   # (uF - uG_prev) + uG_new   (models.py:82-83, parareal.py:382)
+                _lib.check(lib.nngp_parareal_update(self.n, UF[i + 1].data_ptr(), UG[i + 1].data_ptr(),
+                                                    UG1[i + 1].data_ptr(), U1[i + 1].data_ptr(), stream))
+        return ev.collect().get('G', 0.0)
+
     # --------------------------------------------------------------------------- main loop
     def _parareal(self, model, debug=False, early_stop=None, parall='Serial', store_int=False,
                   **kwargs):
@@ -266,23 +315,14 @@ class Parareal():
                 th0 = torch.tensor(model.draw_thetas(N - I), **f64)
                 nf = model.n_fits
             e_loop = ev.start()
-            for i in range(I, N):
-                eg = ev.start()
-                solver.run_G_batch(t_dev[i:i + 1], t_dev[i + 1:i + 2], Uk1[i:i + 1], out=UGk1[i + 1:i + 2])
-                ev.stop(eg, 'G')
-                if is_nngp:
-                    j = i - I
-                    model.predict_device(Xd, Dd, rows, Uk1[i], th0[j * nf:(j + 1) * nf],
-                                         out=Uk1[i + 1], bias=UGk1[i + 1], stream=stream)
-                else:   # (uF - uG_prev) + uG_new   (models.py:82-83, parareal.py:382)
-                    _lib.check(lib.nngp_parareal_update(n, UF[i + 1].data_ptr(), UGk[i + 1].data_ptr(),
-                                                        UGk1[i + 1].data_ptr(), Uk1[i + 1].data_ptr(), stream))
+            g_s = self._correction_sweep(torch, model, t_dev, I, N, Uk1, UGk1, UF, UGk, Xd, Dd, rows,
+                                         th0 if is_nngp else None, stream)
             ev.stop(e_loop, 'loop')
             u[:, :, k + 1] = Uk1.cpu().numpy()
             ug = UGk1.cpu().numpy()
             te = ev.collect()
-            G_time += te.get('G', 0.0)
-            model.add_pred_time(max(te.get('loop', 0.0) - te.get('G', 0.0), 0.0))
+            G_time += g_s
+            model.add_pred_time(max(te.get('loop', 0.0) - g_s, 0.0))
             if np.any(np.isnan(ug)):
                 raise Exception('NaN values in initial coarse solve - increase Ng!')
             err[:, k] = np.linalg.norm(u[:, :, k + 1] - u[:, :, k], np.inf, 1)   # (:402-403)

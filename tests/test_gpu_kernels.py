@@ -228,10 +228,14 @@ def test_predict_restarts_and_small_training_set(gpu):
     assert np.max(np.abs(got - ora)) <= 1e-12 * max(1e-6, np.max(np.abs(ora)))
 
 
-@pytest.mark.parametrize('m,d,R', [(5, 3, 1), (12, 4, 2), (16, 3, 2), (20, 6, 1), (20, 3, 2), (30, 2, 2)])
+@pytest.mark.parametrize('m,d,R', [(5, 3, 1), (12, 4, 2), (16, 3, 2), (20, 6, 1), (20, 3, 2), (30, 2, 2),
+                                   (10, 300, 1), (18, 130, 2)])
 def test_predict_every_padded_size_and_fallback_vs_oracle(gpu, m, d, R):
-    """Fits run padded to 8/16/24/32 rows (identity pad, exact); m > 16 with 2 restarts exceeds
-    one workgroup per coordinate and takes the unfused fits + arg-min/mean path.  Bitwise."""
+    """Fits run padded to 8/16/24/32 rows (identity pad, exact).  Up to 8 fits per CU each fit
+    gets a wave and evaluates reflect/expand/contract points speculatively; above that (d=300:
+    2 700 fits) the packed kernel runs 4 fits per wave, fused with the arg-min and mean -- or,
+    when a coordinate's fits exceed a workgroup (m=18, R=2 at d=130: 4 680 fits), as fits +
+    arg-min/mean kernels.  Every path is bitwise the oracle."""
     import torch
     rng = np.random.default_rng(m * 10 + d + R)
     X = np.cumsum(0.05 * rng.standard_normal((3 * m, d)), axis=0)
