@@ -505,7 +505,7 @@ static const double LOG_2PI = 1.8378770664093453; /* np.log(2*np.pi) */
 
 /* -LML, models.py:240-252 (NaN -> +inf).  jit = 10**jitter (host pow).                       */
 double orc_nlml(int m, const double *D2, const double *y, double sx, double sy, double jit) {
-    double L[64 * 64], alpha[64], tmp[64];
+    double L[64 * 64], alpha[64], tmp[64] = {0};
     const double c = -0.5 * (1 / nn_pow10(sx));
     const double psy = nn_pow10(sy);
     if (gp_factor(m, D2, y, c, psy, jit, L, alpha)) return INFINITY;
@@ -521,7 +521,7 @@ double orc_nlml(int m, const double *D2, const double *y, double sx, double sy, 
 /* posterior mean K(xm, new_x)^T alpha, models.py:162-168                                     */
 double orc_gp_mean_one(int m, const double *D2, const double *kd2, const double *y, double sx,
                        double sy, double jit) {
-    double L[64 * 64], alpha[64], tmp[64];
+    double L[64 * 64], alpha[64], tmp[64] = {0};
     const double c = -0.5 * (1 / nn_pow10(sx));
     const double psy = nn_pow10(sy);
     if (gp_factor(m, D2, y, c, psy, jit, L, alpha)) return NAN;

@@ -11,7 +11,7 @@
 using namespace nngp;
 
 template <int MAXM>
-__global__ void eval_loop(int m, const double *D2, const double *Y, int reps, double *out, long long *cyc) {
+__global__ void __launch_bounds__(64) eval_loop(int m, const double *D2, const double *Y, int reps, double *out, long long *cyc) {
     constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG;
     __shared__ double sD2[32 * 32];
     __shared__ double sK[4 * GP<32>::IMG];
