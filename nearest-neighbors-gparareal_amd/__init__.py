@@ -1,7 +1,7 @@
 """nnGParareal on MI355X: the reference's Parareal / SolverRK / NNGP_p plugin surface with the
 fine RK propagator and the nearest-neighbour GP correction as hand-written HIP kernels for gfx950
 (csrc/, C-ABI in include/nngp.h).  Import as `nngp_amd` (see nngp_amd.py at the repo root)."""
-from . import _lib
+from . import _lib, legacy
 from ._lib import NNGPError, build, lib
 from .configs import Config
 from .models import BareParareal, ModelAbstr, NNGP_p

@@ -68,6 +68,16 @@ class ModelAbstr():
     def predict(self, new_x, prev_F, prev_G):
         raise Exception('Not implemented')
 
+    def state_dict(self):
+        """Counters for a store_int checkpoint (JSON-serialisable)."""
+        return {'name': self.name, 'train_time': self.train_time, 'pred_time': self.pred_time,
+                'pred_times': self.pred_times.tolist(), 'time_k': self.time_k, 'settings': {}}
+
+    def load_state(self, st):
+        self.train_time, self.pred_time = st['train_time'], st['pred_time']
+        self.pred_times = np.array(st['pred_times'], dtype=float)
+        self.time_k = st['time_k']
+
     def store(self):
         if hasattr(self, 'pool'):
             pool = self.pool
@@ -244,6 +254,19 @@ class NNGP_p(ModelAbstr):
         new.pool = None
         new._dev_xy = None
         return new
+
+    def state_dict(self):
+        st = super().state_dict()
+        st['settings'] = {'theta': self.theta.tolist(), 'fatol': self.fatol, 'xatol': self.xatol,
+                          'n_restarts': self.n_restarts, 'nn': self.nn, 'seed': self.seed}
+        st.update({'k': self.k, 'tot_train_t': self.tot_train_t, 'train_count': self.train_count,
+                   'rng': self.rng.bit_generator.state})
+        return st
+
+    def load_state(self, st):
+        super().load_state(st)
+        self.k, self.tot_train_t, self.train_count = st['k'], st['tot_train_t'], st['train_count']
+        self.rng.bit_generator.state = st['rng']
 
     def restore_attrs(self, pool):
         self.pool = pool

@@ -17,6 +17,8 @@ The returned dict has the reference's keys ('t', 'u', 'err', 'x', 'D', 'k', 'dat
 'timings', 'debug_dict', 'converged', 'conv_int').
 """
 import ctypes
+import json
+import os
 import time
 import warnings
 
@@ -168,6 +170,58 @@ class Parareal():
         self.runs[cstm_mdl_name] = out
         return out
 
+    # ------------------------------------------------------------------------ checkpoints
+    def store(self, name, path='', mdl=None, objs=None):
+        """Checkpoint (parareal.py:114-139).  The reference pickles the whole Parareal object;
+        here the arrays go to `<path>/<name>.npz` and everything else (scalars, the model's
+        settings, counters and its np.random.Generator state) to a JSON string inside it, so a
+        checkpoint is loadable with numpy's safe loader (allow_pickle=False)."""
+        if path and not os.path.exists(path):
+            os.makedirs(path)
+        arrays, meta = {}, {'format': 'nngp_amd-int-1', 'ode_name': self.ode_name, 'N': self.N,
+                            'n': self.n, 'epsilon': self.epsilon, 'tspan': list(map(float, self.tspan))}
+        for key, val in (objs or {}).items():
+            if isinstance(val, np.ndarray):
+                arrays[key] = val
+            else:
+                meta[key] = val.item() if isinstance(val, np.generic) else val
+        if mdl is not None:
+            meta['model'] = mdl.state_dict()
+        arrays['meta'] = np.array(json.dumps(meta))
+        np.savez(os.path.join(path, name + '.npz'), **arrays)
+
+    @staticmethod
+    def read_int_dump(file):
+        """Load a store_int checkpoint written by `store` (numpy safe loader, no pickle)."""
+        with np.load(file if file.endswith('.npz') else file + '.npz', allow_pickle=False) as z:
+            state = {k: z[k] for k in z.files if k != 'meta'}
+            state.update(json.loads(str(z['meta'])))
+        return state
+
+    def load_int_dump(self, other, cstm_mdl_name=None, add_model=False, **kwargs):
+        """Resume a run from a store_int checkpoint (parareal.py:141-209): `other` is the
+        checkpoint file (or its already-read state).  The model is rebuilt with its settings,
+        counters and RNG state, so the resumed run draws exactly the stream it would have drawn."""
+        state = other if isinstance(other, dict) else self.read_int_dump(other)
+        if state['ode_name'] != self.ode_name or int(state['n']) != self.n or int(state['N']) != self.N:
+            raise Exception('Input and previous ODEs do not match')
+        mst = state['model']
+        if mst['name'] == 'NNGP':
+            mdl = NNGP_p(n=self.n, N=self.N, worker_pool=GpuPool(), **mst['settings'])
+        else:
+            mdl = BareParareal(N=self.N)
+        mdl.load_state(mst)
+        base_time = float(state['F_time']) + float(state['G_time']) + mdl.get_times()['mdl_tot_t']
+        run_kwargs = dict(kwargs)
+        run_kwargs.setdefault('pool', GpuPool())
+        s_time = time.time()
+        out = self._parareal(mdl, _resume=state, **run_kwargs)
+        out['timings']['runtime'] = time.time() - s_time + base_time
+        if add_model:
+            out['mdl'] = mdl.store()
+        self.runs[cstm_mdl_name or mdl.name] = out
+        return out
+
     # ------------------------------------------------------------------------------ F sweep
     def _fine_sweep(self, torch, t_dev, Uk, UF, I, N, n):
         """uF[I+1:N+1] = F(u[I:N]) -- sharded over ranks when a process group is active."""
@@ -182,7 +236,7 @@ class Parareal():
         solver, lib = self.solver, _lib.lib()
         if N <= I:
             return 0.0
-        if solver.Ng > solver.thresh:   # paged coarse solve (never in the reference configs)
+        if solver.coarse_is_paged():   # paged coarse solve (never in the reference configs)
             return self._correction_sweep_py(torch, model, t_dev, I, N, U1, UG1, UF, UG, X, Y, rows,
                                              th0, stream)
         cs = solver.f.csystem(U1.device)
@@ -225,12 +279,10 @@ class Parareal():
 
     # --------------------------------------------------------------------------- main loop
     def _parareal(self, model, debug=False, early_stop=None, parall='Serial', store_int=False,
-                  **kwargs):
+                  _resume=None, **kwargs):
         torch = _lib.require_gpu()
         if debug:
             warnings.warn('debug mode (per-slice fine re-solves) is not supported; ignored')
-        if store_int:
-            warnings.warn('store_int checkpoints are not implemented yet (SURVEY.md §8f row 4); ignored')
         tspan, N, epsilon, n = self.tspan, self.N, self.epsilon, self.n
         solver = self.solver
         verbose = kwargs.get('verbose', self.verbose)
@@ -259,21 +311,39 @@ class Parareal():
         UF = torch.empty((N + 1, n), **f64)
         UGk[0] = u0
         UF[0] = u0
-        # initial coarse sweep, sequential (parareal.py:265-270)
-        e0 = ev.start()
-        for i in range(N):
-            solver.run_G_batch(t_dev[i:i + 1], t_dev[i + 1:i + 2], UGk[i:i + 1], out=UGk[i + 1:i + 2])
-        ev.stop(e0, 'G')
-        Uk.copy_(UGk)
-        u[:, :, 0] = Uk.cpu().numpy()
-        G_time += ev.collect().get('G', 0.0)
+        if _resume is None:
+            # initial coarse sweep, sequential (parareal.py:265-270; legacy: one global grid,
+            # new_lib.py:902-906 -- the solver decides)
+            e0 = ev.start()
+            solver.initial_coarse(t_dev, UGk, N)
+            ev.stop(e0, 'G')
+            Uk.copy_(UGk)
+            u[:, :, 0] = Uk.cpu().numpy()
+            G_time += ev.collect().get('G', 0.0)
+            k_start = 0
+        else:   # continue from a store_int checkpoint (parareal.py:141-209, 279-297)
+            kc = int(_resume['k'])
+            I, conv_int = int(_resume['I']), [int(c) for c in _resume['conv_int']]
+            u[:, :, :kc + 2] = _resume['u']
+            err[:, :kc + 1] = _resume['err']
+            x, D = np.array(_resume['x']), np.array(_resume['D'])
+            data_x[..., :kc + 1] = _resume['data_x']
+            data_D[..., :kc + 1] = _resume['data_D']
+            G_time, F_time = float(_resume['G_time']), float(_resume['F_time'])
+            F_time_serial = float(_resume['F_time_serial'])
+            Uk.copy_(torch.tensor(u[:, :, kc + 1], **f64))
+            UGk.copy_(torch.tensor(_resume['uG_cur'], **f64))
+            k_start = kc + 1
 
-        cap = max(4 * N, 64)
+        cap = max(4 * N, 64, 2 * x.shape[0])
         Xd = torch.empty((cap, n), **f64)
         Dd = torch.empty((cap, n), **f64)
-        rows = 0
-        k = 0
-        for k in range(N):
+        rows = x.shape[0]
+        if rows:
+            Xd[:rows] = torch.tensor(x, **f64)
+            Dd[:rows] = torch.tensor(D, **f64)
+        k = k_start
+        for k in range(k_start, N):
             if verbose == 'v':
                 print(f'{self.ode_name} {model.name} iteration number (out of {N}): {k + 1} ')
             e0 = ev.start()
@@ -310,12 +380,19 @@ class Parareal():
                 err[-1, k] = np.nextafter(epsilon, 0)
                 break
 
-            model.fit_timed(x, D, k=k, data_x=data_x, data_y=data_D)
+            lag_k = kwargs.get('lag_k')
+            if lag_k is None:
+                model.fit_timed(x, D, k=k, data_x=data_x, data_y=data_D)
+                Xs, Ds, rows_s = Xd, Dd, rows
+            else:   # legacy: train on the last lag_k iterations only (new_lib.py:980-987)
+                tr_x = np.moveaxis(data_x[I:, :, max(k + 1 - lag_k, 0):k + 1], 1, -1).reshape(-1, n)
+                tr_y = np.moveaxis(data_D[I:, :, max(k + 1 - lag_k, 0):k + 1], 1, -1).reshape(-1, n)
+                model.fit_timed(tr_x, tr_y, k=k)
+                Xs, Ds, rows_s = torch.tensor(tr_x, **f64), torch.tensor(tr_y, **f64), tr_x.shape[0]
             if is_nngp:
                 th0 = torch.tensor(model.draw_thetas(N - I), **f64)
-                nf = model.n_fits
             e_loop = ev.start()
-            g_s = self._correction_sweep(torch, model, t_dev, I, N, Uk1, UGk1, UF, UGk, Xd, Dd, rows,
+            g_s = self._correction_sweep(torch, model, t_dev, I, N, Uk1, UGk1, UF, UGk, Xs, Ds, rows_s,
                                          th0 if is_nngp else None, stream)
             ev.stop(e_loop, 'loop')
             u[:, :, k + 1] = Uk1.cpu().numpy()
@@ -337,6 +414,14 @@ class Parareal():
                 print('--> Converged:', I)
             conv_int.append(I)
             Uk, UGk = Uk1, UGk1
+            if store_int:   # parareal.py:420-431 (npz + JSON instead of a pickle of the object)
+                name_base = kwargs.get('int_name', f'{self.ode_name}_{self.N}_{model.name}_int')
+                objs = {'t': t, 'I': I, 'k': k, 'conv_int': np.array(conv_int), 'u': u[..., :k + 2],
+                        'uG_cur': ug, 'err': err[:, :k + 1], 'x': x, 'D': D, 'data_x': data_x[..., :k + 1],
+                        'data_D': data_D[..., :k + 1], 'G_time': G_time, 'F_time': F_time,
+                        'F_time_serial': F_time_serial, 'epsilon': epsilon, 'N': N,
+                        'ode_name': self.ode_name}
+                self.store(name=f'{name_base}_{k}', path=kwargs.get('int_dir', ''), mdl=model, objs=objs)
             if I == N:
                 break
             if (early_stop is not None) and k == (early_stop - 1):

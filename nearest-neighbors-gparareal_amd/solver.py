@@ -127,6 +127,15 @@ class SolverRK(SolverAbstr):
             t1 = torch.tensor(np.asarray(t1, dtype=float), device=U0.device)
         return self._launch(method, t0, t1, steps, U0, out, stream)
 
+    def coarse_is_paged(self):
+        return self.Ng > self.thresh
+
+    def initial_coarse(self, t_dev, UG, N):
+        """Initial coarse sweep (parareal.py:265-270): UG[i+1] = G(t[i], t[i+1], UG[i]), one
+        slice after the other."""
+        for i in range(N):
+            self.run_G_batch(t_dev[i:i + 1], t_dev[i + 1:i + 2], UG[i:i + 1], out=UG[i + 1:i + 2])
+
     def run_F_batch(self, t0, t1, U0, out=None, stream=None):
         return self._run_batch(self.F, self.Nf, t0, t1, U0, out, stream)
 

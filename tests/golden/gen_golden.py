@@ -319,6 +319,27 @@ def part_preds():
          fit_res=c['res'], rnd=c['rnd'], xm=c['xm'], ym=c['ym'])
 
 
+def part_legacy():
+    """The legacy monolith (new_lib.Parareal, the API of every published scalability run): total
+    step counts, per-slice np.linspace grids, one global initial coarse grid, and RK_last's paging
+    quirk with float page lengths (RK_thresh = Nf/N/2.5 -> pages of 180, 180, 90 step-units, each
+    re-using the full 450-step count)."""
+    import new_lib as rnl
+    arrs = {}
+    s = rnl.Parareal(ode_name='lorenz_n', epsilon=5e-7, verbose=None)
+    s.RK_thresh = s.Nf / s.N / 2.5
+    st = time.time()
+    res = s.run(model='parareal')
+    print('legacy parareal paged K=', res['k'], f'{time.time()-st:.1f}s', flush=True)
+    _dump_run('lorenz_para_paged', res, arrs)
+    s = rnl.Parareal(ode_name='lorenz_n', epsilon=5e-7, verbose=None)
+    st = time.time()
+    res = s.run(model='nngp', nn=10, seed=45, early_stop=3)
+    print('legacy nngp 3 iterations', f'{time.time()-st:.1f}s', flush=True)
+    _dump_run('lorenz_nngp3', res, arrs)
+    save('legacy.npz', **arrs)
+
+
 def part_rng():
     rng = np.random.default_rng(45)
     a = np.array([rng.integers(-8, 0, 2) for _ in range(300)])

@@ -81,3 +81,43 @@ def test_solver_rejects_unknown_tableau():
         nngp_amd.SolverRK(f, 6, 45, 'RK3', 'RK4')
     with pytest.raises(TypeError):
         nngp_amd.SolverRK(lambda t, u: u, 6, 45, 'RK4', 'RK4')
+
+
+def test_store_int_checkpoint_round_trip_without_gpu(tmp_path):
+    """Checkpoints are npz + JSON (numpy safe loader, no pickle): arrays, scalars and the
+    model's RNG state survive a round trip, and the restored RNG continues the same stream."""
+    import nngp_amd
+    ode = nngp_amd.Lorenz(normalization='-11')
+    s = nngp_amd.SolverRK(ode.get_vector_field(), Ng=6, Nf=45, F='RK4', G='RK4')
+    p = nngp_amd.Parareal(ode, s, [0, 18], 4, verbose=None)
+    mdl = nngp_amd.NNGP_p(n=3, N=4, nn=10, seed=47)
+    mdl.draw_thetas(2)
+    objs = {'I': 2, 'k': 1, 'conv_int': np.array([1, 2]), 'u': np.arange(30.0).reshape(5, 3, 2),
+            'G_time': 0.5, 'F_time': np.float64(1.5)}
+    p.store(name='ck', path=str(tmp_path), mdl=mdl, objs=objs)
+    st = p.read_int_dump(str(tmp_path / 'ck'))
+    assert st['I'] == 2 and st['k'] == 1 and st['F_time'] == 1.5 and st['ode_name'] == 'Lorenz'
+    assert np.array_equal(st['u'], objs['u']) and list(st['conv_int']) == [1, 2]
+    m2 = nngp_amd.NNGP_p(n=3, N=4, **st['model']['settings'])
+    m2.load_state(st['model'])
+    assert np.array_equal(m2.draw_thetas(3), mdl.draw_thetas(3))
+    with np.load(str(tmp_path / 'ck.npz'), allow_pickle=False) as z:   # loadable without pickle
+        assert 'meta' in z.files
+
+
+def test_legacy_systems_registry_restates_new_lib():
+    import nngp_amd
+    f, tspan, u0, eps, N, Ng, Nf, G, F, tr, tr_inv = nngp_amd.legacy.Systems('lorenz_n').fetch()
+    assert (tspan, eps, N, Ng, Nf, G, F) == ([0, 18], 1e-8, 50, 300, 22500, 'RK4', 'RK4')
+    assert np.allclose(tr_inv(u0), [-15, -15, 20])
+    f, tspan, u0, eps, N, Ng, Nf, G, F, _, _ = nngp_amd.legacy.Systems('non_aut128_n').fetch()
+    assert (tspan, N, Ng, Nf, G, F) == ([-20, 500], 128, 2048, 174080, 'RK1', 'RK8')
+    with pytest.raises(Exception):
+        nngp_amd.legacy.Systems('nosuch')
+    # RK_last's paging schedule (new_lib.py:59-66) incl. a float remainder page
+    from nngp_amd.legacy import _legacy_pages
+    assert _legacy_pages(451, 1e7) is None
+    iters, pts = _legacy_pages(451, 450 / 2.5)
+    assert pts == 450 and iters == [180.0, 180.0, 90.0]
+    with pytest.raises(Exception):
+        nngp_amd.legacy.LegacySolverRK(f, 7, 100, 1000, 'RK4', 'RK1')   # Ng % N != 0
