@@ -13,16 +13,19 @@
 //                      y[:, c] columns and builds D2 = pairwise |xm_r - xm_j|^2 (numpy pairwise
 //                      order) and kd2 = |xm_r - new_x|^2, all theta-independent (hoisted out of
 //                      the ~10^2 likelihood evaluations each fit makes).
-//   nm_fit_kernel<G>   one GROUP of G = 16 or 32 lanes per fit (m <= G), lane r owns row r of the
-//                      m x m kernel matrix in VGPRs.  Each evaluation builds the row
-//                      (10^sy exp(c D2) + jitter I), runs a left-looking Cholesky whose row
-//                      broadcasts are wave shuffles, forward/back triangular solves, and the
-//                      -LML with xor-butterfly reductions.  Nelder-Mead itself is an in-register
-//                      state machine (scipy's rules) so every group of a wave always performs
-//                      exactly one evaluation per loop trip -- no divergent evaluation code.
-//                      FUSED: a workgroup holds whole coordinates, so after a __syncthreads the
-//                      first group of each coordinate does the arg-min and the posterior mean and
-//                      writes preds (+ uG bias = the Parareal update, parareal.py:382).
+//   nm_spec_kernel<MAXM>  one WAVE per fit; its four 16-lane DPP rows evaluate the reflection,
+//                      expansion and both contractions of a Nelder-Mead iteration (or the initial
+//                      simplex / the shrink points) in one round, consumed in scipy's order by the
+//                      unchanged state machine -- identical fits in ~1.5x fewer sequential rounds.
+//   nm_fit_kernel<MAXM, FUSED>  four fits per wave (one DPP row each), one evaluation per trip;
+//                      FUSED: a workgroup holds whole coordinates and its first row per
+//                      coordinate does the arg-min, the posterior mean and u = mean + uG
+//                      (parareal.py:382).  Used when the fits would oversubscribe the SIMDs.
+//   gp_mean_kernel<MAXM>  arg-min (from a fits array) or given (theta, jitter), posterior mean.
+// A likelihood evaluation (gp_factor/gp_nlml): lane l of a fit's row holds rows l (and l+16) of
+// the m x m kernel matrix, padded to MAXM in {8,16,24,32} with exact identity rows; the triangle's
+// exps are spread over the 16 lanes through an LDS image; the Cholesky / solve broadcasts are
+// `v_mov_b64_dpp row_newbcast` (no LDS round trip); the -LML sums are DPP butterflies.
 // Numerics: -ffp-contract=off; orders documented in oracle/nngp_oracle.c, which restates the
 // same arithmetic on the CPU so GPU-vs-oracle parity is (near) bitwise.
 

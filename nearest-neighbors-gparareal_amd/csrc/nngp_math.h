@@ -92,4 +92,59 @@ __device__ __forceinline__ double nn_log(double x_in) {
     return x_in == 0.0 ? -__builtin_huge_val() : (x_in > 0.0 ? x_in : __builtin_nan(""));
 }
 
+// sin / cos for the trigonometric vector fields (ThomasLabyrinth systems.py:257-271, DblPend
+// :182-189), fully specified like exp/log above so the GPU and the oracle agree bit for bit:
+// x = n pi/2 + r by a three-term fma Cody-Waite reduction (fdlibm's 33-bit pi/2 pieces; exact
+// n*PIO2_1 for |n| < 2^20), then fdlibm's __kernel_sin / __kernel_cos polynomials on |r| <= pi/4
+// and the quadrant select.  ~1 ulp for the |x| < 1e5 these fields see.
+struct TrigC {
+    static constexpr double INVPIO2 = 6.36619772367581382433e-01;
+    static constexpr double PIO2_1 = 1.57079632673412561417e+00;
+    static constexpr double PIO2_2 = 6.07710050630396597660e-11;
+    static constexpr double PIO2_3 = 2.02226624871116645580e-21;
+    static constexpr double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                            S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                            S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    static constexpr double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                            C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                            C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+};
+
+__device__ __forceinline__ void nn_sincos(double x, double &sn, double &cs) {
+    const bool fin = x - x == 0.0;                 // finite
+    const double xf = fin ? x : 0.0;
+    const double n = rint(xf * TrigC::INVPIO2);
+    double r = fma(-n, TrigC::PIO2_1, xf);
+    r = fma(-n, TrigC::PIO2_2, r);
+    r = fma(-n, TrigC::PIO2_3, r);
+    const double z = r * r;
+    const double v = z * r;
+    const double ps = TrigC::S2 + z * (TrigC::S3 + z * (TrigC::S4 + z * (TrigC::S5 + z * TrigC::S6)));
+    const double ks = r + v * (TrigC::S1 + z * ps);
+    const double pc = z * (TrigC::C1 + z * (TrigC::C2 + z * (TrigC::C3 + z * (TrigC::C4 + z * (TrigC::C5 + z * TrigC::C6)))));
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double kc = w + (((1.0 - w) - hz) + z * pc);
+    const int q = ((int)(n - 4.0 * floor(n * 0.25))) & 3;
+    double s_ = (q & 1) ? kc : ks;
+    double c_ = (q & 1) ? ks : kc;
+    s_ = (q & 2) ? -s_ : s_;
+    c_ = ((q + 1) & 2) ? -c_ : c_;
+    const double nanv = x - x;                     // NaN for inf / NaN arguments
+    sn = fin ? s_ : nanv;
+    cs = fin ? c_ : nanv;
+}
+
+__device__ __forceinline__ double nn_sin(double x) {
+    double s, c;
+    nn_sincos(x, s, c);
+    return s;
+}
+
+__device__ __forceinline__ double nn_cos(double x) {
+    double s, c;
+    nn_sincos(x, s, c);
+    return c;
+}
+
 }  // namespace nngp

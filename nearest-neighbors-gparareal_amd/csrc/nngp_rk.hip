@@ -22,6 +22,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "nngp_math.h"
 #include "tableau.h"
 
 namespace nngp {
@@ -68,9 +69,9 @@ template <> struct LaneSys<NNGP_SYS_HOPF> {     // systems.py:148-154
 template <> struct LaneSys<NNGP_SYS_THOMAS_LABYRINTH> {   // systems.py:257-271
     static constexpr int D = 3;
     __device__ static void f(const double *u, double *o, const LaneArgs &) {
-        o[0] = -0.5 * u[0] + 10.0 * sin(u[1]);
-        o[1] = -0.5 * u[1] + 10.0 * sin(u[2]);
-        o[2] = -0.5 * u[2] + 10.0 * sin(u[0]);
+        o[0] = -0.5 * u[0] + 10.0 * nn_sin(u[1]);
+        o[1] = -0.5 * u[1] + 10.0 * nn_sin(u[2]);
+        o[2] = -0.5 * u[2] + 10.0 * nn_sin(u[0]);
     }
 };
 template <> struct LaneSys<NNGP_SYS_FHN_ODE> {  // systems.py:87-95 (u**3 = u*(u*u), jax)
@@ -99,13 +100,14 @@ template <> struct LaneSys<NNGP_SYS_BRUSSELATOR> {  // systems.py:209-214
 template <> struct LaneSys<NNGP_SYS_DBL_PEND> {  // systems.py:182-189
     static constexpr int D = 4;
     __device__ static void f(const double *u, double *o, const LaneArgs &) {
-        const double c = cos(u[0] - u[2]), s = sin(u[0] - u[2]);
+        double s, c;
+        nn_sincos(u[0] - u[2], s, c);
+        const double s0 = nn_sin(u[0]), s2 = nn_sin(u[2]);
         const double pre = -1 / (2 - c * c);
         o[0] = u[1];
-        o[1] = pre * ((((u[1] * u[1]) * c) * s + (u[3] * u[3]) * s) + 2 * sin(u[0]) - c * sin(u[2]));
+        o[1] = pre * ((((u[1] * u[1]) * c) * s + (u[3] * u[3]) * s) + 2 * s0 - c * s2);
         o[2] = u[3];
-        o[3] = pre * ((((-2 * (u[1] * u[1])) * s - ((u[3] * u[3]) * s) * c) - (2 * c) * sin(u[0])) +
-                      2 * sin(u[2]));
+        o[3] = pre * ((((-2 * (u[1] * u[1])) * s - ((u[3] * u[3]) * s) * c) - (2 * c) * s0) + 2 * s2);
     }
 };
 

@@ -54,6 +54,11 @@ typedef struct {
     double b[MAXS];
 } tableau_t;
 
+/* fully specified sin/cos (defined below, restating csrc/nngp_math.h) */
+void nn_sincos(double x, double *sn, double *cs);
+double nn_sin(double x);
+double nn_cos(double x);
+
 static void make_tableau(int order, tableau_t *T) {
     memset(T, 0, sizeof(*T));
     if (order == 1) {
@@ -196,9 +201,9 @@ static void rhs_raw(const nngp_system *sys, const double *u, double *out) {
     }
     case NNGP_SYS_THOMAS_LABYRINTH: {
         const double a = 0.5, b = 10.0;
-        out[0] = -a * u[0] + b * sin(u[1]);
-        out[1] = -a * u[1] + b * sin(u[2]);
-        out[2] = -a * u[2] + b * sin(u[0]);
+        out[0] = -a * u[0] + b * nn_sin(u[1]);
+        out[1] = -a * u[1] + b * nn_sin(u[2]);
+        out[2] = -a * u[2] + b * nn_sin(u[0]);
         break;
     }
     case NNGP_SYS_FHN_ODE: {
@@ -219,14 +224,14 @@ static void rhs_raw(const nngp_system *sys, const double *u, double *out) {
         out[1] = 3 * u[0] - (u[0] * u[0]) * u[1];
         break;
     case NNGP_SYS_DBL_PEND: {
-        const double c = cos(u[0] - u[2]), s = sin(u[0] - u[2]);
+        double s, c;
+        nn_sincos(u[0] - u[2], &s, &c);
+        const double s0 = nn_sin(u[0]), s2 = nn_sin(u[2]);
         const double pre = -1 / (2 - c * c);
         out[0] = u[1];
-        out[1] = pre * ((((u[1] * u[1]) * c) * s + (u[3] * u[3]) * s) + 2 * sin(u[0]) -
-                        c * sin(u[2]));
+        out[1] = pre * ((((u[1] * u[1]) * c) * s + (u[3] * u[3]) * s) + 2 * s0 - c * s2);
         out[2] = u[3];
-        out[3] = pre * ((((-2 * (u[1] * u[1])) * s - ((u[3] * u[3]) * s) * c) -
-                         (2 * c) * sin(u[0])) + 2 * sin(u[2]));
+        out[3] = pre * ((((-2 * (u[1] * u[1])) * s - ((u[3] * u[3]) * s) * c) - (2 * c) * s0) + 2 * s2);
         break;
     }
     case NNGP_SYS_BURGERS:
@@ -402,6 +407,53 @@ double nn_log(double x) {   /* fdlibm e_log.c */
     const double R = t2 + t1;
     const double hfsq = 0.5 * f * f;
     return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+/* sin / cos, restating csrc/nngp_math.h nn_sincos bit for bit (fdlibm pieces, fma reduction).  */
+static const double TR_INVPIO2 = 6.36619772367581382433e-01, TR_PIO2_1 = 1.57079632673412561417e+00,
+                    TR_PIO2_2 = 6.07710050630396597660e-11, TR_PIO2_3 = 2.02226624871116645580e-21;
+static const double TR_S1 = -1.66666666666666324348e-01, TR_S2 = 8.33333333332248946124e-03,
+                    TR_S3 = -1.98412698298579493134e-04, TR_S4 = 2.75573137070700676789e-06,
+                    TR_S5 = -2.50507602534068634195e-08, TR_S6 = 1.58969099521155010221e-10;
+static const double TR_C1 = 4.16666666666666019037e-02, TR_C2 = -1.38888888888741095749e-03,
+                    TR_C3 = 2.48015872894767294178e-05, TR_C4 = -2.75573143513906633035e-07,
+                    TR_C5 = 2.08757232129817482790e-09, TR_C6 = -1.13596475577881948265e-11;
+
+void nn_sincos(double x, double *sn, double *cs) {
+    const int fin = (x - x) == 0.0;
+    const double xf = fin ? x : 0.0;
+    const double n = rint(xf * TR_INVPIO2);
+    double r = fma(-n, TR_PIO2_1, xf);
+    r = fma(-n, TR_PIO2_2, r);
+    r = fma(-n, TR_PIO2_3, r);
+    const double z = r * r;
+    const double v = z * r;
+    const double ps = TR_S2 + z * (TR_S3 + z * (TR_S4 + z * (TR_S5 + z * TR_S6)));
+    const double ks = r + v * (TR_S1 + z * ps);
+    const double pc = z * (TR_C1 + z * (TR_C2 + z * (TR_C3 + z * (TR_C4 + z * (TR_C5 + z * TR_C6)))));
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double kc = w + (((1.0 - w) - hz) + z * pc);
+    const int q = ((int)(n - 4.0 * floor(n * 0.25))) & 3;
+    double s_ = (q & 1) ? kc : ks;
+    double c_ = (q & 1) ? ks : kc;
+    s_ = (q & 2) ? -s_ : s_;
+    c_ = ((q + 1) & 2) ? -c_ : c_;
+    const double nanv = x - x;
+    *sn = fin ? s_ : nanv;
+    *cs = fin ? c_ : nanv;
+}
+
+double nn_sin(double x) {
+    double s, c;
+    nn_sincos(x, &s, &c);
+    return s;
+}
+
+double nn_cos(double x) {
+    double s, c;
+    nn_sincos(x, &s, &c);
+    return c;
 }
 
 /* ------------------------------------------------------------------------------------------ */

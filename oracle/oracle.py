@@ -75,7 +75,7 @@ def lib():
                                   _dp, _dp, i32]
         L.orc_d2.argtypes = [_dp, i32, i32, _dp]
         L.orc_max_threads.restype = ctypes.c_int
-        for fn in ('nn_exp', 'nn_log', 'nn_pow10'):
+        for fn in ('nn_exp', 'nn_log', 'nn_pow10', 'nn_sin', 'nn_cos'):
             getattr(L, fn).argtypes = [dbl]
             getattr(L, fn).restype = dbl
         _lib = L
@@ -236,8 +236,11 @@ def predict(X, Y, q, m, theta0, n_restarts=1, fatol=0.1, xatol=0.1, maxfev=400, 
 # ---------------------------------------------------------------------------------------------
 def parareal(system, tspan, N, Ng, Nf, G, F, epsilon=5e-7, model='parareal', nn=10, seed=45,
              n_restarts=1, fatol=0.1, xatol=0.1, u0=None, step_mode=STEP_FIXED, nthreads=0,
-             early_stop=None):
-    """Returns dict(k, u, err, conv_int, converged, x, D) like Parareal._parareal."""
+             early_stop=None, coarse_grid=False):
+    """Returns dict(k, u, err, conv_int, converged, x, D) like Parareal._parareal.  Ng/Nf are
+    per-slice step counts; coarse_grid=True takes the legacy initial coarse solution from one
+    global grid of N*Ng steps (new_lib.py:902-906) -- with step_mode=STEP_LINSPACE this is the
+    legacy new_lib.Parareal loop (unpaged)."""
     n = system.d
     order = {'RK1': 1, 'RK2': 2, 'RK4': 4, 'RK8': 8}
     oG, oF = order[G], order[F]
@@ -256,7 +259,10 @@ def parareal(system, tspan, N, Ng, Nf, G, F, epsilon=5e-7, model='parareal', nn=
     uF[0] = u[0]
     temp = u0
     for i in range(N):                                  # parareal.py:265-270
-        temp = system.rk(oG, t[i], t[i + 1], Ng, temp, step_mode)
+        if coarse_grid:                                 # new_lib.py:902-906
+            temp = system.rk_grid(oG, t[0], t[-1], N * Ng, i * Ng, Ng, temp)
+        else:
+            temp = system.rk(oG, t[i], t[i + 1], Ng, temp, step_mode)
         uG[i + 1, :, 0] = temp
     u[:, :, 0] = uG[:, :, 0]
     I = 0

@@ -325,6 +325,7 @@ def part_legacy():
     quirk with float page lengths (RK_thresh = Nf/N/2.5 -> pages of 180, 180, 90 step-units, each
     re-using the full 450-step count)."""
     import new_lib as rnl
+    rnl.NNGP_p.kernel_jit = staticmethod(_broadcast_kernel)   # same speed substitution as above
     arrs = {}
     s = rnl.Parareal(ode_name='lorenz_n', epsilon=5e-7, verbose=None)
     s.RK_thresh = s.Nf / s.N / 2.5

@@ -87,3 +87,33 @@ def test_burgers_n128_k_in_published_distribution(gpu, seed):
     p = gpu.Parareal(ode, s, [0, 5], 128, epsilon=5e-7, verbose=None)
     r = p.run(model='nngp', nn=15, seed=seed)
     assert r['converged'] and r['k'] in (9, 10)
+
+
+def test_tomlab_nngp_bitwise_equals_oracle_loop(gpu):
+    """ThomasLabyrinth (TomLab.py settings: RK4/RK1, m=18, fatol=xatol=1e-3) on a short span: the
+    sin-based field and the m=18 fits (24-row padded kernel) match the oracle's loop bit for bit."""
+    ode = gpu.ThomasLabyrinth(normalization='-11')
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=10, Nf=200, F='RK4', G='RK1')
+    p = gpu.Parareal(ode, s, [0, 10], 16, epsilon=5e-7, verbose=None)
+    kw = dict(nn=18, n_restarts=1, fatol=1e-3, xatol=1e-3, seed=45, early_stop=4)
+    r = p.run(model='nngp', **kw)
+    so = O.System('tomlab')
+    o = O.parareal(so, [0, 10], 16, 10, 200, 'RK1', 'RK4', model='nngp', nn=18, seed=45, fatol=1e-3,
+                   xatol=1e-3, u0=so.fit([4.6722764, 5.2437205e-10, -6.4444208e-10]), early_stop=4)
+    assert r['k'] == o['k'] and r['conv_int'] == o['conv_int']
+    assert np.array_equal(np.nan_to_num(r['u'], nan=7.0), np.nan_to_num(o['u'], nan=7.0))
+
+
+def test_burgers_n128_first_iteration_bitwise_equals_oracle(gpu):
+    """BASELINE configs[2] (Burgers d=128, N=128, RK8 2000/RK1 4 per slice, m=15): the first
+    iteration -- 128 fine solves and 127 sequential corrections of 1 152 fits each -- is bitwise
+    the oracle's (the bench times the same iteration on the CPU)."""
+    ode = gpu.Burgers(d_x=128, normalization='-11')
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
+    r = gpu.Parareal(ode, s, [0, 5], 128, epsilon=5e-7, verbose=None).run(model='nngp', nn=15, seed=45,
+                                                                          early_stop=1)
+    so = O.System('burgers', d=128, param=(0.01,), mn=0.0, mx=1.0)
+    x = np.linspace(-1, 1, 128)
+    o = O.parareal(so, [0, 5], 128, 4, 2000, 'RK1', 'RK8', model='nngp', nn=15, seed=45,
+                   u0=so.fit(0.5 * (np.cos(4.5 * np.pi * x) + 1)), early_stop=1)
+    assert np.array_equal(np.nan_to_num(r['u'], nan=7.0), np.nan_to_num(o['u'], nan=7.0))

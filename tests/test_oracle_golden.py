@@ -17,7 +17,7 @@ from scipy.optimize import minimize
 
 import oracle as O
 from conftest import golden
-from systems_table import EXACT, KEYS, RK_KEYS, oracle_system
+from systems_table import EXACT, KEYS, RK_KEYS, TRIG, oracle_system
 
 
 @pytest.mark.parametrize('key', KEYS)
@@ -28,6 +28,8 @@ def test_rhs_matches_reference(key):
     out = np.array([s.rhs(u) for u in U])
     if key in EXACT:
         assert np.array_equal(out, F)
+    elif key in TRIG:   # fully specified sin/cos vs the reference's libm: a few ulps
+        assert np.max(np.abs(out - F)) <= 8 * np.spacing(max(1.0, np.max(np.abs(F))))
     else:
         assert np.max(np.abs(out - F)) <= 1e-12 * max(1.0, np.max(np.abs(F)))
 
@@ -46,7 +48,8 @@ def test_rk_matches_reference(key, tab):
         if key in EXACT:
             assert np.array_equal(got, ref)
         else:
-            assert np.max(np.abs(got - ref)) <= 1e-14 * max(1.0, np.max(np.abs(ref)))
+            tol = 1e-13 if key in TRIG else 1e-14
+            assert np.max(np.abs(got - ref)) <= tol * max(1.0, np.max(np.abs(ref)))
 
 
 def test_fixed_and_linspace_differ_only_by_roundoff():
@@ -78,7 +81,7 @@ def test_global_grid_is_the_linspace_grid():
 
 
 def test_math_accuracy():
-    """The shared exp / log / 10^x (GPU csrc/nngp_math.h == oracle) stay within 2 ulp of glibc."""
+    """The shared exp / log / 10^x / sin / cos (GPU csrc/nngp_math.h == oracle) stay within 2 ulp of glibc."""
     L = O.lib()
     rng = np.random.default_rng(0)
     xs = np.concatenate([rng.uniform(-745, 709, 20000), rng.uniform(-1, 1, 20000), [0.0, -0.0, 1e-300]])
@@ -95,6 +98,12 @@ def test_math_accuracy():
     got = np.array([L.nn_log(x) for x in ls])
     assert np.max(np.abs(got - np.log(ls)) / np.spacing(np.abs(np.log(ls)))) <= 2
     assert L.nn_log(0.0) == -np.inf and np.isnan(L.nn_log(-1.0))
+    xs = np.concatenate([rng.uniform(-40, 40, 20000), rng.uniform(-1e4, 1e4, 2000), [0.0, np.pi / 2, -np.pi]])
+    for fn, ref in (('nn_sin', np.sin), ('nn_cos', np.cos)):
+        got = np.array([getattr(L, fn)(x) for x in xs])
+        r = ref(xs)
+        assert np.max(np.abs(got - r) / np.maximum(np.spacing(np.abs(r)), np.spacing(1.0) * 2 ** -10)) <= 2, fn
+    assert np.isnan(L.nn_sin(np.inf)) and np.isnan(L.nn_cos(np.nan))
 
 
 def test_nlml_matches_reference():
