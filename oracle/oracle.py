@@ -285,6 +285,7 @@ def parareal(system, tspan, N, Ng, Nf, G, F, epsilon=5e-7, model='parareal', nn=
                 preds = uF[i + 1, :, k] - uG[i + 1, :, k]           # models.py:82-83
             else:
                 m = max(10, k + 2) if nn == 'adaptive' else nn      # models.py:172-175
+                m = min(m, x.shape[0])            # argsort(...)[:nn] keeps every row if fewer
                 nf = n * len(JITTERS) * n_restarts
                 th0 = rng.integers(-8, 0, (nf, 2)).astype(float)    # models.py:192 (same stream)
                 preds = predict(x, D, u[i, :, k + 1], m, th0, n_restarts, fatol, xatol, nthreads=nthreads)
