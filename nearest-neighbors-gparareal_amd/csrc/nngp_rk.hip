@@ -377,6 +377,88 @@ __global__ void __launch_bounds__(256) rk_field_kernel(FieldArgs fa, int n_slice
 }
 
 // ---------------------------------------------------------------------------------------------
+// Burgers with d = 64*EPT: ONE WAVE per slice, no LDS, no barriers.
+// Lane l owns the contiguous elements l*EPT .. l*EPT+EPT-1; the periodic stencil's outer
+// neighbours come from lanes l-1 / l+1 by `wave_ror:1` / `wave_rol:1` DPP moves, which wrap around
+// the wave exactly like the periodic boundary wraps around the grid.  The general kernel above
+// pays an LDS round trip and a workgroup barrier per stage instead (11 per RK8 step).
+// Summation order = burgers_elem (systems.py:421-446, non-zeros in ascending column order): the
+// three Laplacian terms of rows 0 and d-1 associate differently from the interior rows, so the
+// operands are selected per element; the two gradient terms commute (a+b == b+a bitwise).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_prev(double v) {   // lane i <- lane i-1 (lane 0 <- 63)
+    return __builtin_amdgcn_mov_dpp(v, 0x13C, 0xF, 0xF, false);
+}
+__device__ __forceinline__ double wave_next(double v) {   // lane i <- lane i+1 (lane 63 <- 0)
+    return __builtin_amdgcn_mov_dpp(v, 0x134, 0xF, 0xF, false);
+}
+
+template <int ORDER, bool LINSPACE, int EPT, bool NORM>
+__global__ void __launch_bounds__(64) rk_burgers_wave_kernel(FieldArgs fa, int n_slices,
+                                                              const double *__restrict__ t0,
+                                                              const double *__restrict__ t1,
+                                                              int64_t steps, int64_t gsteps,
+                                                              const int64_t *__restrict__ j0s,
+                                                              const double *__restrict__ u0,
+                                                              double *__restrict__ uF) {
+    using T = Tableau<ORDER>;
+    constexpr int S = T::S;
+    constexpr int d = 64 * EPT;
+    const int slice = blockIdx.x;
+    const int l = threadIdx.x;
+    double u[EPT], k[S * EPT], mn[EPT], w[EPT], sc[EPT];
+#pragma unroll
+    for (int r = 0; r < EPT; r++) {
+        const int e = l * EPT + r;
+        u[r] = u0[(size_t)slice * d + e];
+        mn[r] = NORM ? fa.norm[e] : 0.0;
+        w[r] = NORM ? 0.5 * fa.norm[d + e] : 1.0;   // (mx-mn)/2, see lane_rhs
+        sc[r] = NORM ? fa.norm[2 * d + e] : 1.0;
+    }
+    const bool first = l == 0, last = l == 63;     // rows 0 and d-1 live in lanes 0 and 63
+    const double cxx = fa.c_off, cdg = fa.c_diag, q = fa.c_grad;
+    const double T0 = t0[slice], T1 = t1[slice];
+    const double dt = (T1 - T0) / (double)(LINSPACE ? gsteps : steps);
+    const int64_t j0 = j0s ? j0s[slice] : 0;
+    for (int64_t n = 0; n < steps; n++) {
+        const double h = step_size(LINSPACE, n, j0, gsteps, T0, T1, dt);
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+            double V[EPT];
+#pragma unroll
+            for (int r = 0; r < EPT; r++) {
+                const double x = stage_input<T, EPT>(s, u[r], k, r);
+                V[r] = NORM ? (x + 1) * w[r] + mn[r] : x;
+            }
+            const double Vl = wave_prev(V[EPT - 1]);   // element l*EPT - 1
+            const double Vr = wave_next(V[0]);         // element l*EPT + EPT
+#pragma unroll
+            for (int r = 0; r < EPT; r++) {
+                const double L = r > 0 ? V[r - 1] : Vl;
+                const double C = V[r];
+                const double R = r < EPT - 1 ? V[r + 1] : Vr;
+                const double pL = cxx * L, pC = cdg * C, pR = cxx * R;
+                // row 0: (cdg C + cxx R) + cxx L; row d-1: (cxx R + cxx L) + cdg C; else
+                // (cxx L + cdg C) + cxx R
+                const bool b0 = (r == 0) && first, b1 = (r == EPT - 1) && last;
+                const double a1 = b0 ? pC : (b1 ? pR : pL);
+                const double a2 = b0 ? pR : (b1 ? pL : pC);
+                const double a3 = b0 ? pL : (b1 ? pC : pR);
+                const double lap = (a1 + a2) + a3;
+                const double grad = (-q) * L + q * R;
+                double f = lap - C * grad;
+                if (NORM) f = f * sc[r];
+                k[s * EPT + r] = h * f;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < EPT; r++) u[r] = step_update<T, EPT>(u[r], k, r);   // RK.py:170
+    }
+#pragma unroll
+    for (int r = 0; r < EPT; r++) uF[(size_t)slice * d + l * EPT + r] = u[r];
+}
+
+// ---------------------------------------------------------------------------------------------
 // single RHS evaluations (ODE.get_vector_field()(t, u)) and the elementwise Parareal update
 // ---------------------------------------------------------------------------------------------
 template <int SYS>
@@ -519,6 +601,19 @@ static int field_args(const nngp_system *sys, FieldArgs &fa) {
     return NNGP_OK;
 }
 
+template <int ORDER, bool LIN, int EPT>
+static int launch_burgers_wave(const FieldArgs &fa, int n, const double *t0, const double *t1, int64_t steps,
+                               int64_t gsteps, const int64_t *j0, const double *u0, double *uF, hipStream_t st) {
+    if (fa.normalized)
+        hipLaunchKernelGGL((rk_burgers_wave_kernel<ORDER, LIN, EPT, true>), dim3(n), dim3(64), 0, st, fa, n, t0,
+                           t1, steps, gsteps, j0, u0, uF);
+    else
+        hipLaunchKernelGGL((rk_burgers_wave_kernel<ORDER, LIN, EPT, false>), dim3(n), dim3(64), 0, st, fa, n, t0,
+                           t1, steps, gsteps, j0, u0, uF);
+    NNGP_LAUNCH_CHECK();
+    return NNGP_OK;
+}
+
 template <int SYS, int ORDER, bool LIN>
 static int launch_field(const nngp_system *sys, int n, const double *t0, const double *t1,
                         int64_t steps, int64_t gsteps, const int64_t *j0, const double *u0, double *uF,
@@ -526,6 +621,13 @@ static int launch_field(const nngp_system *sys, int n, const double *t0, const d
     FieldArgs fa;
     int rc = field_args(sys, fa);
     if (rc) return rc;
+    if (SYS == NNGP_SYS_BURGERS && sys->d % 64 == 0 && sys->d <= 256 && !getenv("NNGP_BURGERS_LDS")) {
+        const int e = sys->d / 64;
+        if (e == 1) return launch_burgers_wave<ORDER, LIN, 1>(fa, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+        if (e == 2) return launch_burgers_wave<ORDER, LIN, 2>(fa, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+        if (e == 3) return launch_burgers_wave<ORDER, LIN, 3>(fa, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+        return launch_burgers_wave<ORDER, LIN, 4>(fa, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    }
     const int bt = pick_threads(sys->d);
     const int ept = (sys->d + bt - 1) / bt;
     NNGP_REQUIRE(ept <= 8, "d=%d too large for the field kernel (max 2048)", sys->d);
