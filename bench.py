@@ -196,6 +196,41 @@ def burgers_cpu_iter1(threads):
     return time.perf_counter() - t0, r
 
 
+def burgers_published_schedule(torch, g, sample_pages=2):
+    """The published Burgers N=128 scalability run (Burgers.py:29-33, 95-108: Nf = N*4*10^4 total
+    RK8 steps, RK_thresh = Nf/N/200) pages every slice into 200 pages that each re-use the full
+    39 999-step count (new_lib.py:57-69): 7 999 800 RK8 steps per slice per
+    iteration.  Time `sample_pages` of those pages for all 128 slices (LINSPACE grids, as the
+    legacy RK_last integrates) and scale to the iteration; the reference's own F time per
+    iteration on 128 worker cores was 372.8 s."""
+    ode = g.Burgers(d_x=128, normalization='-11')
+    solver = g.SolverRK(ode.get_vector_field(), Ng=4, Nf=39999, F='RK8', G='RK1', step_mode='linspace',
+                        thresh=float('inf'))
+    n, pages = 128, 200
+    t = np.linspace(0, 5, n + 1)
+    step = (t[1:] - t[:-1]) / 40000
+    dev = lambda a: torch.tensor(a, dtype=torch.float64, device='cuda')
+    U = dev(np.tile(ode.get_init_cond(), (n, 1)))
+    out = torch.empty_like(U)
+    solver.run_F_batch(dev(t[:-1]), dev(t[:-1] + step * 200), U, out=out)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    ts = t[:-1].copy()
+    for _ in range(sample_pages):
+        te = ts + step * 200
+        solver.run_F_batch(dev(ts), dev(te), U, out=out)
+        U, out = out, U
+        ts = te
+    b.record()
+    torch.cuda.synchronize()
+    per_page = a.elapsed_time(b) / 1e3 / sample_pages
+    it = per_page * pages
+    return {'F_per_iteration_s': it, 'reference_F_per_iteration_s': 372.8, 'speedup_vs_reference_F': 372.8 / it,
+            'steps_per_slice': pages * 39999, 'sample': f'{sample_pages} of {pages} pages x 128 slices, RK8, linspace',
+            'us_per_step': per_page / 39999 * 1e6}
+
+
 def read_traffic():
     path = os.path.join(ROOT, 'profiles', 'fine_kernel_traffic.json')
     if os.path.exists(path):
@@ -253,6 +288,7 @@ def main():
             res[f'{which}_n128_to_convergence'] = {'wall_s': wall, 'K': k, 'converged': conv,
                                                    'F_time_s': tim['F_time'], 'mdl_time_s': tim['mdl_tot_t']}
             log(which, 'converged', conv, 'K', k, f'{wall:.2f}s')
+        res['burgers_n128_published_schedule'] = burgers_published_schedule(torch, g)
         res['cpu_baseline'] = cpu_baseline(args.steps_per_slice, args.slices_per_gpu)
         # north-star target (>= 10x the CPU path on Burgers N=128, identical K): time the first
         # iteration on both sides and extrapolate the CPU to the GPU run's K
