@@ -169,7 +169,14 @@ int nngp_predict(const double *X, const double *Y, int64_t rows, int d, const do
  * theta0 = the (N-I) predictions' initial thetas back to back, [(N-I)][d*n_jitter*n_restarts][2]).
  * All slice launches are queued on `stream` without host synchronisation.
  *   t: DEVICE [N+1]; U1, UG1: DEVICE [N+1][d] (rows I.. read, rows I+1.. written);
- *   UF, UG: DEVICE [N+1][d] (parareal model only); preds_scratch: DEVICE [d] (nngp only);
+ *   UF, UG: DEVICE [N+1][d] (parareal model; for nngp they enable speculation);
+ *   preds_scratch: DEVICE [d] (nngp only);
+ *   speculate (nngp): -1 auto, 0 off, 1 on.  Every slice's query is guessed by the classic
+ *     Parareal update along the coarse chain and all their fits run as ONE batched launch; a
+ *     slice whose actual ordered kNN list equals its guess reuses those fits (bitwise identical:
+ *     a fit depends only on the ordered neighbours, coordinate, jitter and theta0), the others
+ *     are recomputed in the sweep.  Auto speculates while (N-I)*d*n_jitter*n_restarts <= 262144.
+ *   spec_hits_out: HOST, number of slices served by the speculative batch, or NULL;
  *   g_ms_out: HOST, total device time of the G launches (ms), or NULL (no timing events).    */
 #define NNGP_MODEL_PARAREAL 0
 #define NNGP_MODEL_NNGP 1
@@ -178,7 +185,8 @@ int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mode
                           const double *UG, int model, const double *X, const double *Y, int64_t rows,
                           int m, int n_jitter, const double *jitter_exp_host, int n_restarts,
                           const double *theta0, double fatol, double xatol, int maxfev,
-                          double *preds_scratch, float *g_ms_out, void *stream);
+                          double *preds_scratch, int speculate, int32_t *spec_hits_out, float *g_ms_out,
+                          void *stream);
 
 #ifdef __cplusplus
 }

@@ -73,7 +73,7 @@ def lib():
                                _vp, _vp, _vp, _vp]
     L.nngp_correction_sweep.argtypes = [ctypes.POINTER(CSystem), i32, i32, i64, _vp, i32, i32, _vp, _vp, _vp,
                                         _vp, i32, _vp, _vp, i64, i32, i32, _dp, i32, _vp, dbl, dbl, i32,
-                                        _vp, ctypes.POINTER(ctypes.c_float), _vp]
+                                        _vp, i32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_float), _vp]
     for name in EXPORTS:
         if name not in ('nngp_abi_version', 'nngp_last_error', 'nngp_device_count'):
             getattr(L, name).restype = i32

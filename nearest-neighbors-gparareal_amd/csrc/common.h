@@ -43,8 +43,21 @@ void set_error(const char *fmt, ...);
         }                                                                                    \
     } while (0)
 
-// Grow-only device scratch owned by the library (one per device), so that steady-state
-// calls never allocate.  Not thread-safe across host threads sharing a device.
-void *workspace(size_t bytes, int *err);
+// Grow-only device scratch owned by the library (per device and slot), so that steady-state
+// calls never allocate.  Slot 0: per-call scratch (nngp_knn / nngp_predict / ...); slot 1: the
+// speculative sweep's batch buffers, which must outlive the per-slice calls.  Growing a slot
+// frees the old buffer after hipFree's implicit device synchronisation.  Not thread-safe across
+// host threads sharing a device.
+constexpr int N_WS_SLOTS = 3;   // slot 2: the sweep's speculation buffers
+void *workspace(size_t bytes, int *err, int slot = 0);
+
+int predict_impl(const double *X, const double *Y, int64_t rows, int d, const double *new_x, int m,
+                 int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
+                 double fatol, double xatol, int maxfev, double *preds_out, const double *bias,
+                 double *out, double *fits_out, const int32_t *spec_idx, const double *spec_fits,
+                 int32_t *hit_flag, hipStream_t st);
+int spec_batch(const double *X, const double *Y, int64_t rows, int d, const double *Q, int nq, int m,
+               int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
+               double fatol, double xatol, int maxfev, int32_t *idx_out, double *fits_out, hipStream_t st);
 
 }  // namespace nngp

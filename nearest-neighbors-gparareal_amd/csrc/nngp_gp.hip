@@ -129,11 +129,14 @@ __device__ double pw_sqdiff(const double *__restrict__ a, const double *__restri
 // ---------------------------------------------------------------------------------------------
 // kNN
 // ---------------------------------------------------------------------------------------------
+// blockIdx.y = query (batched: query y is q + y*d, its distances dist + y*rows)
 __global__ void __launch_bounds__(64) knn_dist_kernel(const double *__restrict__ X, int64_t rows,
                                                       int d, const double *__restrict__ q,
                                                       double *__restrict__ dist) {
     __shared__ double tile[64][65];   // +1 pad: lane l reads row l -> distinct banks
     __shared__ double qs[64];
+    q += (size_t)blockIdx.y * d;
+    dist += (size_t)blockIdx.y * rows;
     const int lane = threadIdx.x;
     const int64_t r0 = (int64_t)blockIdx.x * 64;
     double acc = 0.0;
@@ -163,16 +166,26 @@ __global__ void __launch_bounds__(64) knn_dist_kernel(const double *__restrict__
     if (r0 + lane < rows) dist[r0 + lane] = acc;
 }
 
-// one workgroup of 256 threads
+// one workgroup of 256 threads per query (blockIdx.y; batched outputs at query-strided offsets).
+// spec_idx / hit_flag (single query): hit_flag = 1 iff the selected ordered neighbour list equals
+// spec_idx -- the speculative sweep then reuses the fits it computed for that list.
 __global__ void __launch_bounds__(256) knn_select_kernel(
     const double *__restrict__ dist, int64_t rows, int m, const double *__restrict__ X,
     const double *__restrict__ Y, int d, const double *__restrict__ q, int32_t *__restrict__ idx_out,
     double *__restrict__ dist_out, double *__restrict__ ymT, double *__restrict__ D2,
-    double *__restrict__ kd2) {
+    double *__restrict__ kd2, const int32_t *__restrict__ spec_idx, int32_t *__restrict__ hit_flag) {
     __shared__ double wv[4];
     __shared__ int64_t wi[4];
     __shared__ int32_t sel[64];
     __shared__ double seld[64];
+    const int qy = blockIdx.y;
+    dist += (size_t)qy * rows;
+    q += (size_t)qy * d;
+    idx_out += (size_t)qy * m;
+    if (dist_out) dist_out += (size_t)qy * m;
+    if (ymT) ymT += (size_t)qy * d * m;
+    if (D2) D2 += (size_t)qy * m * m;
+    if (kd2) kd2 += (size_t)qy * m;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     double pv = -INFINITY;
     int64_t pi = -1;
@@ -220,6 +233,11 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
         idx_out[k] = sel[k];
         if (dist_out) dist_out[k] = seld[k];
     }
+    if (hit_flag && tid == 0) {
+        int hit = 1;
+        for (int k = 0; k < m; k++) hit &= (sel[k] == spec_idx[k]);
+        *hit_flag = hit;
+    }
     if (ymT) {
         for (int t = tid; t < m * d; t += 256) {
             const int r = t % m, c = t / m;
@@ -237,7 +255,8 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
             D2[r * m + j] = v;
             D2[j * m + r] = v;
         }
-        for (int r = tid; r < m; r += 256) kd2[r] = pw_sqdiff(X + (int64_t)sel[r] * d, q, d);
+        if (kd2)
+            for (int r = tid; r < m; r += 256) kd2[r] = pw_sqdiff(X + (int64_t)sel[r] * d, q, d);
     }
 }
 
@@ -694,7 +713,21 @@ struct NMArgs {
     double *preds;               // FUSED [d]
     const double *bias;          // FUSED [d] or null
     double *out;                 // FUSED [d] (preds + bias) or null
+    // speculative sweep
+    const int32_t *skip;         // fits kernels: if *skip the launch does nothing (speculation hit)
+    const double *fits_alt;      // gp_mean_kernel: arg-min over fits_alt instead if *skip
+    // batched predictions (unfused fits kernel, blockIdx.y = prediction): per-prediction strides
+    int64_t qs_D2, qs_Y, qs_th, qs_fits;
 };
+
+// apply the blockIdx.y prediction offsets of a batched launch (all zero otherwise)
+__device__ __forceinline__ void nm_batch_offsets(NMArgs &a) {
+    const int64_t y = blockIdx.y;
+    a.D2 += y * a.qs_D2;
+    a.Y += y * a.qs_Y;
+    a.theta0 += y * a.qs_th;
+    if (a.fits_out) a.fits_out += y * a.qs_fits;
+}
 
 // static-index lookup (a runtime index into a by-value kernel-argument array would go to scratch)
 __device__ __forceinline__ double jit_lookup(const NMArgs &a, int j) {
@@ -712,6 +745,8 @@ template <int MAXM, bool FUSED>
 __global__ void __launch_bounds__(NMBound<MAXM>::T) nm_fit_kernel(NMArgs a) {
     constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG;
     extern __shared__ __attribute__((aligned(16))) double sm[];
+    if (a.skip && *a.skip) return;   // uniform: the whole grid exits
+    nm_batch_offsets(a);
     const int m = a.m;
     const int nfc = a.nj * a.R;                         // fits per coordinate
     const int galloc = blockDim.x / 16;                 // groups incl. padding lanes
@@ -877,6 +912,7 @@ template <int MAXM>
 __global__ void __launch_bounds__(256) nm_spec_kernel(NMArgs a) {
     constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG;
     extern __shared__ __attribute__((aligned(16))) double sm[];
+    if (a.skip && *a.skip) return;   // uniform: the whole grid exits (speculation hit)
     const int m = a.m;
     const int nfc = a.nj * a.R;
     double *sD2 = sm;
@@ -992,7 +1028,8 @@ __global__ void __launch_bounds__(256) gp_mean_kernel(NMArgs a) {
     int jidx;
     if (a.fits_out) {
         const int nfc = a.nj * a.R;
-        const double *F = a.fits_out + (size_t)4 * cc * nfc;
+        const double *FB = (a.skip && *a.skip) ? a.fits_alt : a.fits_out;
+        const double *F = FB + (size_t)4 * cc * nfc;
         int best = 0;
         double bv = F[2];
         for (int t = 1; t < nfc; t++)
@@ -1035,11 +1072,11 @@ static int maxm_for(int m) { return m <= 8 ? 8 : (m <= 16 ? 16 : (m <= 24 ? 24 :
 static size_t k_image_doubles(int maxm) { return (size_t)16 * (maxm > 16 ? 2 : 1) * (maxm + 1); }
 
 template <int MAXM>
-static int launch_nm(NMArgs &a, bool fused, int nblocks, int threads, size_t lds, hipStream_t st) {
+static int launch_nm(NMArgs &a, bool fused, int nblocks, int threads, size_t lds, hipStream_t st, int nq) {
     if (fused)
         hipLaunchKernelGGL((nm_fit_kernel<MAXM, true>), dim3(nblocks), dim3(threads), lds, st, a);
     else
-        hipLaunchKernelGGL((nm_fit_kernel<MAXM, false>), dim3(nblocks), dim3(threads), lds, st, a);
+        hipLaunchKernelGGL((nm_fit_kernel<MAXM, false>), dim3(nblocks, nq), dim3(threads), lds, st, a);
     NNGP_LAUNCH_CHECK();
     return NNGP_OK;
 }
@@ -1090,7 +1127,7 @@ static bool use_spec(int n_fits) {
     return n_fits <= 8 * ncu;
 }
 
-static int run_nm(NMArgs &a, bool fused, hipStream_t st) {
+static int run_nm(NMArgs &a, bool fused, hipStream_t st, int nq = 1) {
     const int maxm = maxm_for(a.m);
     const size_t kimg = k_image_doubles(maxm);
     const int tmax = maxm <= 16 ? NMBound<16>::T : NMBound<32>::T;
@@ -1123,10 +1160,10 @@ static int run_nm(NMArgs &a, bool fused, hipStream_t st) {
     }
     const size_t lds = lds_of(threads);
     switch (maxm) {
-    case 8: return launch_nm<8>(a, fused, nblocks, threads, lds, st);
-    case 16: return launch_nm<16>(a, fused, nblocks, threads, lds, st);
-    case 24: return launch_nm<24>(a, fused, nblocks, threads, lds, st);
-    default: return launch_nm<32>(a, fused, nblocks, threads, lds, st);
+    case 8: return launch_nm<8>(a, fused, nblocks, threads, lds, st, nq);
+    case 16: return launch_nm<16>(a, fused, nblocks, threads, lds, st, nq);
+    case 24: return launch_nm<24>(a, fused, nblocks, threads, lds, st, nq);
+    default: return launch_nm<32>(a, fused, nblocks, threads, lds, st, nq);
     }
 }
 
@@ -1148,7 +1185,8 @@ extern "C" int nngp_knn(const double *X, int64_t rows, int d, const double *q, i
                        d, q, dist);
     NNGP_LAUNCH_CHECK();
     hipLaunchKernelGGL(knn_select_kernel, dim3(1), dim3(256), 0, st, dist, rows, m, X, (const double *)nullptr,
-                       d, q, idx_out, dist_out, (double *)nullptr, (double *)nullptr, (double *)nullptr);
+                       d, q, idx_out, dist_out, (double *)nullptr, (double *)nullptr, (double *)nullptr,
+                       (const int32_t *)nullptr, (int32_t *)nullptr);
     NNGP_LAUNCH_CHECK();
     return NNGP_OK;
 }
@@ -1205,21 +1243,28 @@ extern "C" int nngp_gp_mean(int m, int d, const double *xm, const double *ym, co
     return run_mean(ma, st);
 }
 
-extern "C" int nngp_predict(const double *X, const double *Y, int64_t rows, int d, const double *new_x,
-                            int m, int n_jitter, const double *jitter_exp_host, int n_restarts,
-                            const double *theta0, double fatol, double xatol, int maxfev,
-                            double *preds_out, const double *bias, double *out, double *fits_out,
-                            void *stream) {
+namespace nngp {
+
+// One prediction (NNGP_p.predict).  With spec_idx (the ordered neighbour list a speculative batch
+// assumed for this query), spec_fits (that batch's fits for it) and hit_flag (device int):
+// knn_select sets *hit_flag = (actual list == spec_idx); the fits launch then exits at once on a
+// hit and the arg-min/mean kernel reads spec_fits -- bitwise what it would have computed, since a
+// fit depends only on (the ordered neighbours, its coordinate, jitter and theta0).
+int predict_impl(const double *X, const double *Y, int64_t rows, int d, const double *new_x, int m,
+                 int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
+                 double fatol, double xatol, int maxfev, double *preds_out, const double *bias,
+                 double *out, double *fits_out, const int32_t *spec_idx, const double *spec_fits,
+                 int32_t *hit_flag, hipStream_t st) {
     NNGP_REQUIRE(X && Y && new_x && theta0 && preds_out, "null array argument");
     NNGP_REQUIRE(m >= 1 && m <= 32, "need 1 <= m <= 32 (got %d)", m);
     NNGP_REQUIRE(m <= rows, "m=%d exceeds training rows=%lld", m, (long long)rows);
     NNGP_REQUIRE(d >= 1 && n_restarts >= 1 && maxfev >= 1, "bad d / n_restarts / maxfev");
-    hipStream_t st = (hipStream_t)stream;
+    const bool spec = spec_idx && spec_fits && hit_flag;
     NMArgs a{};
     int rc = fill_jitters(a, n_jitter, jitter_exp_host);
     if (rc) return rc;
     // workspace: dist[rows] | D2[m*m] | kd2[m] | ymT[d*m] | idx[m] (int32) | fits[n_fits][4]
-    // (the fits scratch serves the unfused fallback below when the caller passes no fits_out)
+    // (the fits scratch serves the unfused paths when the caller passes no fits_out)
     const size_t nd = (size_t)rows + (size_t)m * m + m + (size_t)d * m;
     const size_t n_fits = (size_t)d * n_jitter * n_restarts;
     int err = 0;
@@ -1230,31 +1275,85 @@ extern "C" int nngp_predict(const double *X, const double *Y, int64_t rows, int 
     double *kd2 = D2 + (size_t)m * m;
     double *ymT = kd2 + m;
     int32_t *idx = (int32_t *)(ymT + (size_t)d * m);
+    double *fits_ws = (double *)(ws + sizeof(double) * nd + sizeof(int32_t) * 64);
     hipLaunchKernelGGL(knn_dist_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, X, rows,
                        d, new_x, dist);
     NNGP_LAUNCH_CHECK();
     hipLaunchKernelGGL(knn_select_kernel, dim3(1), dim3(256), 0, st, dist, rows, m, X, Y, d, new_x,
-                       idx, (double *)nullptr, ymT, D2, kd2);
+                       idx, (double *)nullptr, ymT, D2, kd2, spec ? spec_idx : nullptr, spec ? hit_flag : nullptr);
     NNGP_LAUNCH_CHECK();
-    a.m = m; a.d = d; a.n_fits = d * n_jitter * n_restarts;
+    a.m = m; a.d = d; a.n_fits = (int)n_fits;
     a.D2 = D2; a.kd2 = kd2; a.Y = ymT; a.ys_c = m; a.ys_r = 1;
     a.theta0 = theta0; a.fatol = fatol; a.xatol = xatol; a.maxfev = maxfev; a.R = n_restarts;
-    a.fits_out = fits_out; a.preds = preds_out; a.bias = bias; a.out = out;
-    if (!fits_out) a.fits_out = (double *)(ws + sizeof(double) * nd + sizeof(int32_t) * 64);
+    a.fits_out = fits_out ? fits_out : fits_ws;
+    a.preds = preds_out; a.bias = bias; a.out = out;
+    if (spec) {
+        a.skip = hit_flag;
+        a.fits_alt = spec_fits;
+    }
     if (use_spec(a.n_fits)) {   // fits (a wave each), then arg-min + mean (+ bias) per coordinate
         rc = run_nm_spec(a, st);
         if (rc) return rc;
         return run_mean(a, st);
     }
-    a.fits_out = fits_out;
-    rc = run_nm(a, true, st);
-    if (rc != NNGP_E_UNSUPPORTED) return rc;
-    // a coordinate's fits exceed one workgroup (large m with restarts): fits kernel, then the
-    // per-coordinate arg-min + posterior mean kernel
-    if (!fits_out) a.fits_out = (double *)(ws + sizeof(double) * nd + sizeof(int32_t) * 64);
+    if (!spec) {
+        NMArgs fu = a;
+        fu.fits_out = fits_out;
+        rc = run_nm(fu, true, st);
+        if (rc != NNGP_E_UNSUPPORTED) return rc;
+    }
+    // a coordinate's fits exceed one workgroup (large m with restarts), or speculation: fits
+    // kernel, then the per-coordinate arg-min + posterior mean kernel
     NMArgs u = a;
     u.preds = nullptr; u.out = nullptr; u.bias = nullptr;
     rc = run_nm(u, false, st);
     if (rc) return rc;
     return run_mean(a, st);
+}
+
+// The speculative batch: for nq guessed queries Q[nq][d] at once, the ordered kNN lists
+// (idx_out[nq][m]) and every fit of every prediction (fits_out[nq][n_fits][4]), with each
+// prediction's own theta0 draws (theta0[nq][n_fits][2]).  One kNN-distance launch, one
+// kNN-select launch (a workgroup per query) and ONE packed fits launch (4 fits per wave over
+// all nq*n_fits fits) -- the throughput-shaped work that the sequential sweep then only looks up.
+int spec_batch(const double *X, const double *Y, int64_t rows, int d, const double *Q, int nq, int m,
+               int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
+               double fatol, double xatol, int maxfev, int32_t *idx_out, double *fits_out, hipStream_t st) {
+    NNGP_REQUIRE(nq >= 1 && m >= 1 && m <= 32 && m <= rows, "bad speculative batch shape");
+    NMArgs a{};
+    int rc = fill_jitters(a, n_jitter, jitter_exp_host);
+    if (rc) return rc;
+    const size_t nfp = (size_t)d * n_jitter * n_restarts;
+    // slot-1 workspace: dist[nq][rows] | D2[nq][m*m] | ymT[nq][d*m]
+    int err = 0;
+    double *dist = (double *)workspace(sizeof(double) * (size_t)nq * ((size_t)rows + (size_t)m * m + (size_t)d * m),
+                                       &err, 1);
+    if (err) return err;
+    double *D2 = dist + (size_t)nq * rows;
+    double *ymT = D2 + (size_t)nq * m * m;
+    hipLaunchKernelGGL(knn_dist_kernel, dim3((unsigned)((rows + 63) / 64), (unsigned)nq), dim3(64), 0, st, X,
+                       rows, d, Q, dist);
+    NNGP_LAUNCH_CHECK();
+    hipLaunchKernelGGL(knn_select_kernel, dim3(1, (unsigned)nq), dim3(256), 0, st, dist, rows, m, X, Y, d, Q,
+                       idx_out, (double *)nullptr, ymT, D2, (double *)nullptr, (const int32_t *)nullptr,
+                       (int32_t *)nullptr);
+    NNGP_LAUNCH_CHECK();
+    a.m = m; a.d = d; a.n_fits = (int)nfp;
+    a.D2 = D2; a.Y = ymT; a.ys_c = m; a.ys_r = 1;
+    a.theta0 = theta0; a.fatol = fatol; a.xatol = xatol; a.maxfev = maxfev; a.R = n_restarts;
+    a.fits_out = fits_out;
+    a.qs_D2 = (int64_t)m * m; a.qs_Y = (int64_t)d * m; a.qs_th = (int64_t)nfp * 2; a.qs_fits = (int64_t)nfp * 4;
+    return run_nm(a, false, st, nq);
+}
+
+}  // namespace nngp
+
+extern "C" int nngp_predict(const double *X, const double *Y, int64_t rows, int d, const double *new_x,
+                            int m, int n_jitter, const double *jitter_exp_host, int n_restarts,
+                            const double *theta0, double fatol, double xatol, int maxfev,
+                            double *preds_out, const double *bias, double *out, double *fits_out,
+                            void *stream) {
+    return nngp::predict_impl(X, Y, rows, d, new_x, m, n_jitter, jitter_exp_host, n_restarts, theta0, fatol,
+                              xatol, maxfev, preds_out, bias, out, fits_out, nullptr, nullptr, nullptr,
+                              (hipStream_t)stream);
 }

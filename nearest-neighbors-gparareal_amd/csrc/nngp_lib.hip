@@ -21,10 +21,10 @@ struct Ws {
     void *ptr = nullptr;
     size_t bytes = 0;
 };
-static std::vector<Ws> g_ws;
+static std::vector<Ws> g_ws;   // [device * N_WS_SLOTS + slot]
 static std::mutex g_ws_mu;
 
-void *workspace(size_t bytes, int *err) {
+void *workspace(size_t bytes, int *err, int slot) {
     int dev = 0;
     *err = 0;
     if (hipGetDevice(&dev) != hipSuccess) {
@@ -33,8 +33,9 @@ void *workspace(size_t bytes, int *err) {
         return nullptr;
     }
     std::lock_guard<std::mutex> lk(g_ws_mu);
-    if ((int)g_ws.size() <= dev) g_ws.resize(dev + 1);
-    Ws &w = g_ws[dev];
+    const int key = dev * N_WS_SLOTS + slot;
+    if ((int)g_ws.size() <= key) g_ws.resize(key + 1);
+    Ws &w = g_ws[key];
     if (w.bytes < bytes) {
         // grow (x1.5) -- the stream-ordered users are synchronised by hipFree's implicit sync
         if (w.ptr) (void)hipFree(w.ptr);

@@ -130,6 +130,9 @@ class Parareal():
         self.u0 = ode.get_init_cond()
         self.verbose = verbose
         self.process_group = process_group
+        # nnGP sweep speculation (include/nngp.h nngp_correction_sweep): -1 auto, 0 off, 1 on
+        self.speculate = int(kwargs.get('speculate', -1))
+        self.spec_hits = []
 
     def _get_pool(self, *args, **kwargs):
         pool = kwargs.get('pool', None)
@@ -246,17 +249,20 @@ class Parareal():
             jit, jp = _lib.host_doubles(JITTERS)
             if not hasattr(self, '_preds_scratch') or self._preds_scratch.device != U1.device:
                 self._preds_scratch = torch.empty(self.n, dtype=torch.float64, device=U1.device)
+            hits = ctypes.c_int32(0)
             _lib.check(lib.nngp_correction_sweep(
                 ctypes.byref(cs), _lib.TABLEAU[solver.G], solver.step_mode, solver.Ng, t_dev.data_ptr(), I, N,
-                U1.data_ptr(), UG1.data_ptr(), None, None, _lib.MODEL_NNGP, X.data_ptr(), Y.data_ptr(),
-                int(rows), m, len(jit), jp, model.n_restarts, th0.data_ptr(), float(model.fatol),
-                float(model.xatol), model.maxfev, self._preds_scratch.data_ptr(), ctypes.byref(g_ms), stream))
+                U1.data_ptr(), UG1.data_ptr(), UF.data_ptr(), UG.data_ptr(), _lib.MODEL_NNGP, X.data_ptr(),
+                Y.data_ptr(), int(rows), m, len(jit), jp, model.n_restarts, th0.data_ptr(), float(model.fatol),
+                float(model.xatol), model.maxfev, self._preds_scratch.data_ptr(), self.speculate,
+                ctypes.byref(hits), ctypes.byref(g_ms), stream))
             model.train_count += model.n_fits * (N - I)
+            self.spec_hits.append(int(hits.value))
         else:
             _lib.check(lib.nngp_correction_sweep(
                 ctypes.byref(cs), _lib.TABLEAU[solver.G], solver.step_mode, solver.Ng, t_dev.data_ptr(), I, N,
                 U1.data_ptr(), UG1.data_ptr(), UF.data_ptr(), UG.data_ptr(), _lib.MODEL_PARAREAL, None, None,
-                0, 0, 0, None, 0, None, 0.0, 0.0, 0, None, ctypes.byref(g_ms), stream))
+                0, 0, 0, None, 0, None, 0.0, 0.0, 0, None, 0, None, ctypes.byref(g_ms), stream))
         return g_ms.value / 1e3
 
     def _correction_sweep_py(self, torch, model, t_dev, I, N, U1, UG1, UF, UG, X, Y, rows, th0, stream):
@@ -283,6 +289,7 @@ class Parareal():
         torch = _lib.require_gpu()
         if debug:
             warnings.warn('debug mode (per-slice fine re-solves) is not supported; ignored')
+        self.spec_hits = []
         tspan, N, epsilon, n = self.tspan, self.N, self.epsilon, self.n
         solver = self.solver
         verbose = kwargs.get('verbose', self.verbose)
@@ -429,7 +436,8 @@ class Parareal():
                     print('Early stopping due to user condition.')
                 break
 
-        timings = {'F_time': F_time, 'G_time': G_time, 'F_time_serial_avg': F_time_serial}
+        timings = {'F_time': F_time, 'G_time': G_time, 'F_time_serial_avg': F_time_serial,
+                   'spec_hits': list(self.spec_hits)}
         timings.update(model.get_times())
         return {'t': t, 'u': u[:, :, :k + 1], 'err': err[:, :k + 1], 'x': x, 'D': D, 'k': k + 1,
                 'data_x': data_x[..., :k + 1], 'data_D': data_D[..., :k + 1], 'timings': timings,

@@ -117,3 +117,26 @@ def test_burgers_n128_first_iteration_bitwise_equals_oracle(gpu):
     o = O.parareal(so, [0, 5], 128, 4, 2000, 'RK1', 'RK8', model='nngp', nn=15, seed=45,
                    u0=so.fit(0.5 * (np.cos(4.5 * np.pi * x) + 1)), early_stop=1)
     assert np.array_equal(np.nan_to_num(r['u'], nan=7.0), np.nan_to_num(o['u'], nan=7.0))
+
+
+@pytest.mark.parametrize('case', ['burgers', 'lorenz'])
+def test_speculative_sweep_is_bitwise_and_hits(gpu, case):
+    """The speculative sweep (every slice's fits batched up front for a Parareal-guessed query,
+    reused where the actual ordered kNN list matches) changes no bit of the run."""
+    if case == 'burgers':
+        ode = gpu.Burgers(d_x=128, normalization='-11')
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
+        mk = lambda spec: gpu.Parareal(ode, s, [0, 5], 128, epsilon=5e-7, verbose=None, speculate=spec)
+        kw = dict(nn=15, seed=45, early_stop=3)
+    else:
+        ode = gpu.Lorenz(normalization='-11')
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=6, Nf=450, F='RK4', G='RK4')
+        mk = lambda spec: gpu.Parareal(ode, s, [0, 18], 32, epsilon=5e-7, verbose=None, speculate=spec)
+        kw = dict(nn=10, seed=47)
+    a = mk(0).run(model='nngp', **kw)
+    b = mk(1).run(model='nngp', **kw)
+    assert a['k'] == b['k'] and a['conv_int'] == b['conv_int']
+    assert np.array_equal(np.nan_to_num(a['u'], nan=7.0), np.nan_to_num(b['u'], nan=7.0))
+    hits = b['timings']['spec_hits']
+    print(case, 'speculation hits per iteration', hits)
+    assert sum(hits) > 0 and a['timings']['spec_hits'] == [0] * len(hits)
