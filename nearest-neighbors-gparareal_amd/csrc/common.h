@@ -55,9 +55,11 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
                  int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
                  double fatol, double xatol, int maxfev, double *preds_out, const double *bias,
                  double *out, double *fits_out, const int32_t *spec_idx, const double *spec_fits,
-                 int32_t *hit_flag, hipStream_t st);
+                 int32_t *hit_flag, const int32_t *spec2_idx, const double *spec2_fits, int32_t *host_flag,
+                 hipStream_t st);
 int spec_batch(const double *X, const double *Y, int64_t rows, int d, const double *Q, int nq, int m,
                int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
-               double fatol, double xatol, int maxfev, int32_t *idx_out, double *fits_out, hipStream_t st);
+               double fatol, double xatol, int maxfev, int32_t *idx_out, double *fits_out, bool latency,
+               hipStream_t st);
 
 }  // namespace nngp

@@ -47,12 +47,22 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// (value, index) order of numpy argsort with NaN last; strict
-__device__ __forceinline__ bool key_less(double av, int64_t ai, double bv, int64_t bi) {
-    const bool an = av != av, bn = bv != bv;
-    if (an != bn) return bn;
-    if (!an && av != bv) return av < bv;
-    return ai < bi;
+// (value, index) order of numpy argsort with NaN last, on the squared distances the kNN selects
+// from (always >= +0 or NaN): the IEEE bit pattern of a non-negative double orders like its value,
+// and every NaN maps to one key above +inf, so a (u64 key, index) pair compares with integer ops.
+__device__ __forceinline__ uint64_t dist_key(double v) {
+    return (v != v) ? 0x7FF8000000000000ull : (uint64_t)__double_as_longlong(v);
+}
+
+__device__ __forceinline__ bool key_less(uint64_t a, int ai, uint64_t b, int bi) {
+    return (a < b) | ((a == b) & (ai < bi));
+}
+
+// take (k, r) as the running minimum when it is a candidate (r >= 0) ahead of the current one
+__device__ __forceinline__ void key_take(uint64_t &bk, int &bi, uint64_t k, int r) {
+    const bool t = (r >= 0) & ((bi < 0) | key_less(k, r, bk, bi));
+    bk = t ? k : bk;
+    bi = t ? r : bi;
 }
 
 // numpy pairwise_sum of (a[i]-b[i])^2, i < n (numpy/_core/src/umath/loops_utils.h.src)
@@ -129,53 +139,113 @@ __device__ double pw_sqdiff(const double *__restrict__ a, const double *__restri
 // ---------------------------------------------------------------------------------------------
 // kNN
 // ---------------------------------------------------------------------------------------------
-// blockIdx.y = query (batched: query y is q + y*d, its distances dist + y*rows)
+// blockIdx.y = query (batched: query y is q + y*d, its distances dist + y*rows).
+// One lane per training row: the row is read with 16-byte vector loads that are all in flight at
+// once (no LDS staging, no barriers), then summed sequentially in column order (scipy cdist).
 __global__ void __launch_bounds__(64) knn_dist_kernel(const double *__restrict__ X, int64_t rows,
                                                       int d, const double *__restrict__ q,
                                                       double *__restrict__ dist) {
-    __shared__ double tile[64][65];   // +1 pad: lane l reads row l -> distinct banks
-    __shared__ double qs[64];
     q += (size_t)blockIdx.y * d;
     dist += (size_t)blockIdx.y * rows;
-    const int lane = threadIdx.x;
-    const int64_t r0 = (int64_t)blockIdx.x * 64;
+    const int64_t r = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (r >= rows) return;
+    const double *xr = X + r * d;
     double acc = 0.0;
-    if (d <= 8) {   // tiny rows: direct
-        const int64_t r = r0 + lane;
-        if (r < rows)
-            for (int c = 0; c < d; c++) {
-                const double t = q[c] - X[r * d + c];
-                acc = acc + t * t;
+    int c = 0;
+    if ((((uintptr_t)xr | (uintptr_t)q) & 15) == 0) {   // 16-byte aligned rows: double2 loads
+        constexpr int B = 16;                            // 16 loads in flight per lane
+        for (; c + 2 * B <= d; c += 2 * B) {
+            double2 v[B];
+#pragma unroll
+            for (int j = 0; j < B; j++) v[j] = *(const double2 *)(xr + c + 2 * j);
+#pragma unroll
+            for (int j = 0; j < B; j++) {
+                const double t0 = q[c + 2 * j] - v[j].x;
+                acc = acc + t0 * t0;
+                const double t1 = q[c + 2 * j + 1] - v[j].y;
+                acc = acc + t1 * t1;
             }
-    } else {
-        for (int c0 = 0; c0 < d; c0 += 64) {
-            const int nc = min(64, d - c0);
-            for (int rr = 0; rr < 64; rr++) {
-                const int64_t r = r0 + rr;
-                tile[rr][lane] = (r < rows && lane < nc) ? X[r * d + c0 + lane] : 0.0;
-            }
-            qs[lane] = lane < nc ? q[c0 + lane] : 0.0;
-            __syncthreads();
-            for (int c = 0; c < nc; c++) {
-                const double t = qs[c] - tile[lane][c];
-                acc = acc + t * t;
-            }
-            __syncthreads();
         }
     }
-    if (r0 + lane < rows) dist[r0 + lane] = acc;
+    for (; c < d; c++) {
+        const double t = q[c] - xr[c];
+        acc = acc + t * t;
+    }
+    dist[r] = acc;
+}
+
+__device__ __forceinline__ double wave_lane_double(double v, int lane) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+
+// Wave-wide minimum of the (key, index) pair (index -1 = no candidate) with DPP moves inside each
+// 16-lane row (quad_perm 1,0,3,2 / 2,3,0,1, row_half_mirror, row_mirror: after each level every
+// lane of the aligned block holds the block's minimum, so a mirror reaches the partner block) and
+// v_readlane across the four rows.  The order is total, so every lane ends with the same pair.
+template <int CTRL>
+__device__ __forceinline__ void key_min_dpp(uint64_t &bk, int &bi) {
+    const uint32_t lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)bk, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(bk >> 32), CTRL, 0xF, 0xF, false);
+    const int oi = __builtin_amdgcn_mov_dpp(bi, CTRL, 0xF, 0xF, false);
+    key_take(bk, bi, ((uint64_t)hi << 32) | lo, oi);
+}
+
+__device__ __forceinline__ void wave_key_min(uint64_t &bk, int &bi) {
+    key_min_dpp<0xB1>(bk, bi);    // quad_perm [1,0,3,2]
+    key_min_dpp<0x4E>(bk, bi);    // quad_perm [2,3,0,1]
+    key_min_dpp<0x141>(bk, bi);   // row_half_mirror
+    key_min_dpp<0x140>(bk, bi);   // row_mirror
+    uint64_t rk = 0;
+    int ri = -1;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)bk, 16 * r);
+        const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(bk >> 32), 16 * r);
+        key_take(rk, ri, ((uint64_t)hi << 32) | lo, __builtin_amdgcn_readlane(bi, 16 * r));
+    }
+    bk = rk;
+    bi = ri;
+}
+
+// LDS staging of the m selected rows for the pair distances (at most 48 KB; larger m*d reads X)
+static inline int knn_xs_doubles(int m, int64_t d) { return (int64_t)m * d <= 6144 ? (int)(m * d) : 0; }
+static inline size_t knn_xs_bytes(int m, int64_t d) { return (size_t)knn_xs_doubles(m, d) * sizeof(double); }
+
+template <int K> __global__ void knn_select_kernel(const double *, int64_t, int, const double *, const double *, int,
+                                                  const double *, int32_t *, double *, double *, double *,
+                                                  double *, const int32_t *, int32_t *, int, const int32_t *,
+                                                  int32_t *);
+
+// register-resident keys when rows <= 256*K (K = 2..16), else the streaming form (K = 0)
+template <typename... A>
+static void launch_knn_select(dim3 grid, size_t shmem, hipStream_t st, const double *dist, int64_t rows,
+                              A... args) {
+    const int64_t per = (rows + 255) / 256;
+    if (per <= 2)
+        hipLaunchKernelGGL(knn_select_kernel<2>, grid, dim3(256), shmem, st, dist, rows, args...);
+    else if (per <= 4)
+        hipLaunchKernelGGL(knn_select_kernel<4>, grid, dim3(256), shmem, st, dist, rows, args...);
+    else if (per <= 8)
+        hipLaunchKernelGGL(knn_select_kernel<8>, grid, dim3(256), shmem, st, dist, rows, args...);
+    else if (per <= 16)
+        hipLaunchKernelGGL(knn_select_kernel<16>, grid, dim3(256), shmem, st, dist, rows, args...);
+    else
+        hipLaunchKernelGGL(knn_select_kernel<0>, grid, dim3(256), shmem, st, dist, rows, args...);
 }
 
 // one workgroup of 256 threads per query (blockIdx.y; batched outputs at query-strided offsets).
 // spec_idx / hit_flag (single query): hit_flag = 1 iff the selected ordered neighbour list equals
-// spec_idx -- the speculative sweep then reuses the fits it computed for that list.
+// spec_idx, else 2 iff it equals spec2_idx (when given), else 0 -- the speculative sweep then
+// reuses the fits it computed for that list.  host_flag (host-mapped, optional) gets the same value.
+template <int K>
 __global__ void __launch_bounds__(256) knn_select_kernel(
     const double *__restrict__ dist, int64_t rows, int m, const double *__restrict__ X,
     const double *__restrict__ Y, int d, const double *__restrict__ q, int32_t *__restrict__ idx_out,
     double *__restrict__ dist_out, double *__restrict__ ymT, double *__restrict__ D2,
-    double *__restrict__ kd2, const int32_t *__restrict__ spec_idx, int32_t *__restrict__ hit_flag) {
-    __shared__ double wv[4];
-    __shared__ int64_t wi[4];
+    double *__restrict__ kd2, const int32_t *__restrict__ spec_idx, int32_t *__restrict__ hit_flag,
+    int xs_doubles, const int32_t *__restrict__ spec2_idx, int32_t *host_flag) {
     __shared__ int32_t sel[64];
     __shared__ double seld[64];
     const int qy = blockIdx.y;
@@ -187,56 +257,83 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
     if (D2) D2 += (size_t)qy * m * m;
     if (kd2) kd2 += (size_t)qy * m;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    double pv = -INFINITY;
-    int64_t pi = -1;
-    for (int k = 0; k < m; k++) {
-        double bv = 0.0;
-        int64_t bi = -1;
-        for (int64_t r = tid; r < rows; r += 256) {
-            const double v = dist[r];
-            if (!key_less(pv, pi, v, r)) continue;   // must come strictly after previous pick
-            if (bi < 0 || key_less(v, r, bv, bi)) {
-                bv = v;
-                bi = r;
+    // 1) each wave: its m best (value, index) keys among rows wid, wid+4, ... in ascending key
+    //    order, by m rounds of "smallest key strictly after the previous pick" with a
+    //    wave-wide DPP key minimum (no block barriers)
+    __shared__ uint64_t cv[4][64];
+    __shared__ int ci[4][64];
+    {
+        // K > 0: the lane's K keys (rows lane + 64*wid + 256*j) stay in registers for all m rounds
+        uint64_t kv[K > 0 ? K : 1];
+        int kr[K > 0 ? K : 1];
+        if constexpr (K > 0) {
+#pragma unroll
+            for (int j = 0; j < K; j++) {
+                const int r = wid * 64 + lane + 256 * j;
+                kr[j] = r < rows ? r : -1;
+                kv[j] = r < rows ? dist_key(dist[r]) : 0;
             }
         }
-        // wave reduce (xor butterfly on (value, index); no candidate = index -1)
-        for (int s = 1; s < 64; s <<= 1) {
-            const double ov = __shfl_xor(bv, s, 64);
-            const int64_t oi = __shfl_xor(bi, s, 64);
-            if (oi >= 0 && (bi < 0 || key_less(ov, oi, bv, bi))) {
-                bv = ov;
-                bi = oi;
-            }
-        }
-        if (lane == 0) {
-            wv[wid] = bv;
-            wi[wid] = bi;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            double b = wv[0];
-            int64_t bidx = wi[0];
-            for (int w = 1; w < 4; w++)
-                if (wi[w] >= 0 && (bidx < 0 || key_less(wv[w], wi[w], b, bidx))) {
-                    b = wv[w];
-                    bidx = wi[w];
+        uint64_t pk = 0;   // (0, -1) precedes every (key, row >= 0)
+        int pi = -1;
+        for (int k = 0; k < m; k++) {
+            uint64_t bk = 0;
+            int bi = -1;
+            if constexpr (K > 0) {
+#pragma unroll
+                for (int j = 0; j < K; j++)   // strictly after the last pick
+                    key_take(bk, bi, kv[j], key_less(pk, pi, kv[j], kr[j]) ? kr[j] : -1);
+            } else {
+                for (int r = wid * 64 + lane; r < rows; r += 256) {
+                    const uint64_t v = dist_key(dist[r]);
+                    key_take(bk, bi, v, key_less(pk, pi, v, r) ? r : -1);
                 }
-            sel[k] = (int32_t)bidx;
-            seld[k] = b;
+            }
+            wave_key_min(bk, bi);
+            if (lane == 0) {
+                cv[wid][k] = bk;
+                ci[wid][k] = bi;
+            }
+            pk = bk;
+            pi = bi;
         }
-        __syncthreads();
-        pv = seld[k];
-        pi = sel[k];
     }
+    __syncthreads();
+    // 2) wave 0 merges the 4 sorted candidate lists (the global m smallest keys are among them)
+    if (wid == 0) {
+        uint64_t pk = 0;
+        int pi = -1;
+        for (int k = 0; k < m; k++) {
+            uint64_t bk = 0;
+            int bi = -1;
+            for (int t2 = lane; t2 < 4 * m; t2 += 64) {
+                const uint64_t v = cv[t2 / m][t2 % m];
+                const int r = ci[t2 / m][t2 % m];
+                key_take(bk, bi, v, key_less(pk, pi, v, r) ? r : -1);
+            }
+            wave_key_min(bk, bi);
+            if (lane == 0) {
+                sel[k] = (int32_t)bi;
+                seld[k] = __longlong_as_double((long long)bk);
+            }
+            pk = bk;
+            pi = bi;
+        }
+    }
+    __syncthreads();
     for (int k = tid; k < m; k += 256) {
         idx_out[k] = sel[k];
         if (dist_out) dist_out[k] = seld[k];
     }
     if (hit_flag && tid == 0) {
-        int hit = 1;
-        for (int k = 0; k < m; k++) hit &= (sel[k] == spec_idx[k]);
+        int hit1 = 1, hit2 = spec2_idx != nullptr;
+        for (int k = 0; k < m; k++) {
+            hit1 &= (sel[k] == spec_idx[k]);
+            if (spec2_idx) hit2 &= (sel[k] == spec2_idx[k]);
+        }
+        const int hit = hit1 ? 1 : (hit2 ? 2 : 0);
         *hit_flag = hit;
+        if (host_flag) __hip_atomic_store(host_flag, hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (ymT) {
         for (int t = tid; t < m * d; t += 256) {
@@ -245,13 +342,22 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
         }
     }
     if (D2) {
-        // lower triangle incl. diagonal, mirrored ((a-b)^2 == (b-a)^2 bitwise)
+        // lower triangle incl. diagonal, mirrored ((a-b)^2 == (b-a)^2 bitwise); the m neighbour
+        // rows are staged in LDS with coalesced loads when they fit (xs_cap doubles)
+        extern __shared__ __attribute__((aligned(16))) double xs[];
+        const int xs_cap = xs_doubles;
+        const bool staged = (int64_t)m * d <= xs_cap;
+        if (staged)
+            for (int t = tid; t < m * d; t += 256) xs[t] = X[(int64_t)sel[t / d] * d + t % d];
+        __syncthreads();
         const int npairs = m * (m + 1) / 2;
         for (int t = tid; t < npairs; t += 256) {
             int r = 0;
             while ((r + 1) * (r + 2) / 2 <= t) r++;
             const int j = t - r * (r + 1) / 2;
-            const double v = pw_sqdiff(X + (int64_t)sel[r] * d, X + (int64_t)sel[j] * d, d);
+            const double *xr = staged ? xs + (size_t)r * d : X + (int64_t)sel[r] * d;
+            const double *xj = staged ? xs + (size_t)j * d : X + (int64_t)sel[j] * d;
+            const double v = pw_sqdiff(xr, xj, d);
             D2[r * m + j] = v;
             D2[j * m + r] = v;
         }
@@ -715,7 +821,8 @@ struct NMArgs {
     double *out;                 // FUSED [d] (preds + bias) or null
     // speculative sweep
     const int32_t *skip;         // fits kernels: if *skip the launch does nothing (speculation hit)
-    const double *fits_alt;      // gp_mean_kernel: arg-min over fits_alt instead if *skip
+    const double *fits_alt;      // gp_mean_kernel: arg-min over fits_alt instead if *skip == 1,
+    const double *fits_alt2;     //   over fits_alt2 if *skip == 2
     // batched predictions (unfused fits kernel, blockIdx.y = prediction): per-prediction strides
     int64_t qs_D2, qs_Y, qs_th, qs_fits;
 };
@@ -902,17 +1009,12 @@ __device__ __forceinline__ int nm_candidates(const NM &S, NMCand (&c)[4]) {
     }
 }
 
-__device__ __forceinline__ double wave_lane_double(double v, int lane) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
-    return __hiloint2double(hi, lo);
-}
-
 template <int MAXM>
 __global__ void __launch_bounds__(256) nm_spec_kernel(NMArgs a) {
     constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG;
     extern __shared__ __attribute__((aligned(16))) double sm[];
     if (a.skip && *a.skip) return;   // uniform: the whole grid exits (speculation hit)
+    nm_batch_offsets(a);
     const int m = a.m;
     const int nfc = a.nj * a.R;
     double *sD2 = sm;
@@ -1028,7 +1130,8 @@ __global__ void __launch_bounds__(256) gp_mean_kernel(NMArgs a) {
     int jidx;
     if (a.fits_out) {
         const int nfc = a.nj * a.R;
-        const double *FB = (a.skip && *a.skip) ? a.fits_alt : a.fits_out;
+        const int sk = a.skip ? *a.skip : 0;
+        const double *FB = sk == 0 ? a.fits_out : (sk == 2 ? a.fits_alt2 : a.fits_alt);
         const double *F = FB + (size_t)4 * cc * nfc;
         int best = 0;
         double bv = F[2];
@@ -1097,11 +1200,11 @@ static int run_mean(NMArgs &a, hipStream_t st) {
 }
 
 // speculative kernel: one wave per fit, 4 fits per 256-thread workgroup
-static int run_nm_spec(NMArgs &a, hipStream_t st) {
+static int run_nm_spec(NMArgs &a, hipStream_t st, int nq = 1) {
     const int maxm = maxm_for(a.m);
     const int threads = 256;
     const size_t lds = sizeof(double) * ((size_t)a.m * a.m + (size_t)(threads / 16) * k_image_doubles(maxm));
-    const dim3 grid((a.n_fits + threads / 64 - 1) / (threads / 64));
+    const dim3 grid((a.n_fits + threads / 64 - 1) / (threads / 64), nq);
     switch (maxm) {
     case 8: hipLaunchKernelGGL(nm_spec_kernel<8>, grid, dim3(threads), lds, st, a); break;
     case 16: hipLaunchKernelGGL(nm_spec_kernel<16>, grid, dim3(threads), lds, st, a); break;
@@ -1184,9 +1287,9 @@ extern "C" int nngp_knn(const double *X, int64_t rows, int d, const double *q, i
     hipLaunchKernelGGL(knn_dist_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, X, rows,
                        d, q, dist);
     NNGP_LAUNCH_CHECK();
-    hipLaunchKernelGGL(knn_select_kernel, dim3(1), dim3(256), 0, st, dist, rows, m, X, (const double *)nullptr,
-                       d, q, idx_out, dist_out, (double *)nullptr, (double *)nullptr, (double *)nullptr,
-                       (const int32_t *)nullptr, (int32_t *)nullptr);
+    launch_knn_select(dim3(1), 0, st, dist, rows, m, X, (const double *)nullptr, d, q, idx_out, dist_out,
+                      (double *)nullptr, (double *)nullptr, (double *)nullptr, (const int32_t *)nullptr,
+                      (int32_t *)nullptr, 0, (const int32_t *)nullptr, (int32_t *)nullptr);
     NNGP_LAUNCH_CHECK();
     return NNGP_OK;
 }
@@ -1254,7 +1357,8 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
                  int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
                  double fatol, double xatol, int maxfev, double *preds_out, const double *bias,
                  double *out, double *fits_out, const int32_t *spec_idx, const double *spec_fits,
-                 int32_t *hit_flag, hipStream_t st) {
+                 int32_t *hit_flag, const int32_t *spec2_idx, const double *spec2_fits, int32_t *host_flag,
+                 hipStream_t st) {
     NNGP_REQUIRE(X && Y && new_x && theta0 && preds_out, "null array argument");
     NNGP_REQUIRE(m >= 1 && m <= 32, "need 1 <= m <= 32 (got %d)", m);
     NNGP_REQUIRE(m <= rows, "m=%d exceeds training rows=%lld", m, (long long)rows);
@@ -1279,8 +1383,10 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
     hipLaunchKernelGGL(knn_dist_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, X, rows,
                        d, new_x, dist);
     NNGP_LAUNCH_CHECK();
-    hipLaunchKernelGGL(knn_select_kernel, dim3(1), dim3(256), 0, st, dist, rows, m, X, Y, d, new_x,
-                       idx, (double *)nullptr, ymT, D2, kd2, spec ? spec_idx : nullptr, spec ? hit_flag : nullptr);
+    launch_knn_select(dim3(1), knn_xs_bytes(m, d), st, dist, rows, m, X, Y, d, new_x, idx, (double *)nullptr,
+                      ymT, D2, kd2, spec ? spec_idx : (const int32_t *)nullptr,
+                      spec ? hit_flag : (int32_t *)nullptr, knn_xs_doubles(m, d),
+                      spec ? spec2_idx : (const int32_t *)nullptr, spec ? host_flag : (int32_t *)nullptr);
     NNGP_LAUNCH_CHECK();
     a.m = m; a.d = d; a.n_fits = (int)n_fits;
     a.D2 = D2; a.kd2 = kd2; a.Y = ymT; a.ys_c = m; a.ys_r = 1;
@@ -1290,6 +1396,7 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
     if (spec) {
         a.skip = hit_flag;
         a.fits_alt = spec_fits;
+        a.fits_alt2 = spec2_fits;
     }
     if (use_spec(a.n_fits)) {   // fits (a wave each), then arg-min + mean (+ bias) per coordinate
         rc = run_nm_spec(a, st);
@@ -1318,7 +1425,8 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
 // all nq*n_fits fits) -- the throughput-shaped work that the sequential sweep then only looks up.
 int spec_batch(const double *X, const double *Y, int64_t rows, int d, const double *Q, int nq, int m,
                int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
-               double fatol, double xatol, int maxfev, int32_t *idx_out, double *fits_out, hipStream_t st) {
+               double fatol, double xatol, int maxfev, int32_t *idx_out, double *fits_out, bool latency,
+               hipStream_t st) {
     NNGP_REQUIRE(nq >= 1 && m >= 1 && m <= 32 && m <= rows, "bad speculative batch shape");
     NMArgs a{};
     int rc = fill_jitters(a, n_jitter, jitter_exp_host);
@@ -1334,15 +1442,17 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
     hipLaunchKernelGGL(knn_dist_kernel, dim3((unsigned)((rows + 63) / 64), (unsigned)nq), dim3(64), 0, st, X,
                        rows, d, Q, dist);
     NNGP_LAUNCH_CHECK();
-    hipLaunchKernelGGL(knn_select_kernel, dim3(1, (unsigned)nq), dim3(256), 0, st, dist, rows, m, X, Y, d, Q,
-                       idx_out, (double *)nullptr, ymT, D2, (double *)nullptr, (const int32_t *)nullptr,
-                       (int32_t *)nullptr);
+    launch_knn_select(dim3(1, (unsigned)nq), knn_xs_bytes(m, d), st, dist, rows, m, X, Y, d, Q, idx_out,
+                      (double *)nullptr, ymT, D2, (double *)nullptr, (const int32_t *)nullptr,
+                      (int32_t *)nullptr, knn_xs_doubles(m, d), (const int32_t *)nullptr, (int32_t *)nullptr);
     NNGP_LAUNCH_CHECK();
     a.m = m; a.d = d; a.n_fits = (int)nfp;
     a.D2 = D2; a.Y = ymT; a.ys_c = m; a.ys_r = 1;
     a.theta0 = theta0; a.fatol = fatol; a.xatol = xatol; a.maxfev = maxfev; a.R = n_restarts;
     a.fits_out = fits_out;
     a.qs_D2 = (int64_t)m * m; a.qs_Y = (int64_t)d * m; a.qs_th = (int64_t)nfp * 2; a.qs_fits = (int64_t)nfp * 4;
+    // latency: a wave per fit (the re-speculation window the sweep waits on); else packed fits
+    if (latency) return run_nm_spec(a, st, nq);
     return run_nm(a, false, st, nq);
 }
 
@@ -1354,6 +1464,6 @@ extern "C" int nngp_predict(const double *X, const double *Y, int64_t rows, int 
                             double *preds_out, const double *bias, double *out, double *fits_out,
                             void *stream) {
     return nngp::predict_impl(X, Y, rows, d, new_x, m, n_jitter, jitter_exp_host, n_restarts, theta0, fatol,
-                              xatol, maxfev, preds_out, bias, out, fits_out, nullptr, nullptr, nullptr,
-                              (hipStream_t)stream);
+                              xatol, maxfev, preds_out, bias, out, fits_out, nullptr, nullptr, nullptr, nullptr,
+                              nullptr, nullptr, (hipStream_t)stream);
 }

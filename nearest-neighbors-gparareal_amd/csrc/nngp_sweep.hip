@@ -8,6 +8,7 @@
 // nnGP: kNN distance, kNN select, fused fits + arg-min + mean + update).  Driving that chain from
 // Python costs tens of microseconds of interpreter/ctypes work per launch; here the loop issues the
 // launches back to back on one stream, so the GPU never waits for the host.
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -27,6 +28,76 @@ static int timing_events(size_t n, hipEvent_t **out) {
     }
     *out = g_events.data();
     return NNGP_OK;
+}
+
+// re-speculation resources (per process; one device per process): a side stream, the events
+// that order it against the sweep's stream, and host-mapped hit flags the select kernel writes
+struct Respec {
+    int dev = -1;
+    hipStream_t st2 = nullptr;
+    hipEvent_t ev_g = nullptr, ev_r = nullptr;
+    int32_t *hflags = nullptr;   // host-mapped, fine-grained
+    size_t nflags = 0;
+};
+static Respec g_respec;
+static std::mutex g_respec_mu;
+
+static int respec_resources(size_t nflags, Respec **out) {
+    std::lock_guard<std::mutex> lk(g_respec_mu);
+    Respec &r = g_respec;
+    int dev = 0;
+    NNGP_HIP_CHECK(hipGetDevice(&dev));
+    if (r.dev != dev) {   // first use (or another device): fresh stream / events / flags
+        if (r.st2) (void)hipStreamDestroy(r.st2);
+        if (r.ev_g) (void)hipEventDestroy(r.ev_g);
+        if (r.ev_r) (void)hipEventDestroy(r.ev_r);
+        if (r.hflags) (void)hipHostFree(r.hflags);
+        r = Respec{};
+        NNGP_HIP_CHECK(hipStreamCreateWithFlags(&r.st2, hipStreamNonBlocking));
+        NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_g, hipEventDisableTiming));
+        NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_r, hipEventDisableTiming));
+        r.dev = dev;
+    }
+    if (r.nflags < nflags) {
+        if (r.hflags) (void)hipHostFree(r.hflags);
+        r.hflags = nullptr;
+        r.nflags = 0;
+        NNGP_HIP_CHECK(hipHostMalloc((void **)&r.hflags, sizeof(int32_t) * nflags,
+                                     hipHostMallocMapped | hipHostMallocCoherent));
+        r.nflags = nflags;
+    }
+    *out = &r;
+    return NNGP_OK;
+}
+
+// wait for the select kernel's host-mapped hit flag (-1 = not yet written); a stream that has
+// drained (or failed) without writing it is an error, never a hang
+static int wait_flag(const int32_t *flag, hipStream_t st, int32_t *out) {
+    for (uint64_t spin = 1;; spin++) {
+        const int32_t v = __atomic_load_n(flag, __ATOMIC_ACQUIRE);
+        if (v >= 0) {
+            *out = v;
+            return NNGP_OK;
+        }
+        if ((spin & 1023) == 0) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipSuccess && __atomic_load_n(flag, __ATOMIC_ACQUIRE) < 0) {
+                set_error("correction sweep: speculation flag was not written");
+                return NNGP_E_HIP;
+            }
+            if (q != hipSuccess && q != hipErrorNotReady) {
+                set_error("correction sweep: %s", hipGetErrorString(q));
+                return NNGP_E_HIP;
+            }
+        }
+    }
+}
+
+// slices re-speculated after a miss (NNGP_RESPEC_W; 0 disables)
+static int respec_window() {
+    const char *e = getenv("NNGP_RESPEC_W");
+    const int w = e ? atoi(e) : 4;
+    return w < 0 ? 0 : w;
 }
 }  // namespace nngp
 
@@ -76,20 +147,44 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
     // run all of their fits as one batch; the sweep below then only recomputes the slices whose
     // actual ordered neighbour list differs from the guessed one.
     const int64_t nq = N - I;
-    int32_t *spec_idx = nullptr, *flags = nullptr;
-    double *spec_fits = nullptr;
+    int32_t *spec_idx = nullptr, *flags = nullptr, *spec2_idx = nullptr;
+    double *spec_fits = nullptr, *spec2_fits = nullptr, *Qr = nullptr, *gtmp = nullptr;
     const bool spec = model == NNGP_MODEL_NNGP && UF && UG && speculate_ok(speculate, nq, n_fits);
+    // ---- re-speculation: the chain guesses drift; when slice i misses, the next W slices are
+    // guessed again by the same update along the coarse chain, restarted from the actual U1[i]
+    // (its G(U1[i]) is the sweep's own UG1[i+1]), and their fits run as one launch on a side
+    // stream while slice i's own fits run.  Their lists/fits form a second candidate set (hit = 2).
+    const int W = spec ? (int)std::min<int64_t>(respec_window(), nq - 1) : 0;
+    Respec *rs = nullptr;
+    if (W > 0) {
+        const int rc0 = respec_resources((size_t)nq, &rs);
+        if (rc0) return rc0;
+    }
     if (spec) {
         int err = 0;
         const size_t bytes = sizeof(double) * ((size_t)nq * d + d + (size_t)nq * n_fits * 4) +
-                             sizeof(int32_t) * ((size_t)nq * m + nq);
+                             sizeof(int32_t) * ((size_t)nq * m + nq) +
+                             (W > 0 ? sizeof(double) * ((size_t)W * d + d + (size_t)nq * n_fits * 4) +
+                                          sizeof(int32_t) * (size_t)nq * m
+                                    : 0);
         char *ws = (char *)workspace(bytes, &err, 2);
         if (err) return err;
         double *Qg = (double *)ws;
-        double *gtmp = Qg + (size_t)nq * d;
+        gtmp = Qg + (size_t)nq * d;
         spec_fits = gtmp + d;
-        spec_idx = (int32_t *)(spec_fits + (size_t)nq * n_fits * 4);
+        double *tail = spec_fits + (size_t)nq * n_fits * 4;
+        if (W > 0) {
+            Qr = tail;
+            spec2_fits = Qr + (size_t)W * d + d;   // Qr[W][d] | gtmp2[d] | fits
+            tail = spec2_fits + (size_t)nq * n_fits * 4;
+        }
+        spec_idx = (int32_t *)tail;
         flags = spec_idx + (size_t)nq * m;
+        if (W > 0) {
+            spec2_idx = flags + nq;
+            NNGP_HIP_CHECK(hipMemsetAsync(spec2_idx, 0xFF, sizeof(int32_t) * (size_t)nq * m, st));   // -1: none
+            for (int64_t j = 0; j < nq; j++) rs->hflags[j] = -1;
+        }
         NNGP_HIP_CHECK(hipMemcpyAsync(Qg, U1 + (size_t)I * d, sizeof(double) * d, hipMemcpyDeviceToDevice, st));
         for (int64_t j = 0; j + 1 < nq && rc == NNGP_OK; j++) {
             const int i = I + (int)j;
@@ -100,35 +195,69 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
         }
         if (rc == NNGP_OK)
             rc = spec_batch(X, Y, rows, d, Qg, (int)nq, m, n_jitter, jitter_exp_host, n_restarts, theta0, fatol,
-                            xatol, maxfev, spec_idx, spec_fits, st);
+                            xatol, maxfev, spec_idx, spec_fits, false, st);
         if (rc) return rc;
     }
+    bool respec_pending = false;
     for (int i = I; i < N && rc == NNGP_OK; i++) {
         const double *ui = U1 + (size_t)i * d;
         double *ug_next = UG1 + (size_t)(i + 1) * d;
         double *u_next = U1 + (size_t)(i + 1) * d;
-        if (ev) NNGP_HIP_CHECK(hipEventRecord(ev[2 * (i - I)], st));
+        const size_t j = (size_t)(i - I);
+        if (ev) NNGP_HIP_CHECK(hipEventRecord(ev[2 * j], st));
         rc = nngp_rk_batch(sys, g_tableau, g_step_mode, 1, t + i, t + i + 1, g_steps, ui, ug_next, stream);
         if (rc) break;
-        if (ev) NNGP_HIP_CHECK(hipEventRecord(ev[2 * (i - I) + 1], st));
+        if (ev) NNGP_HIP_CHECK(hipEventRecord(ev[2 * j + 1], st));
         if (model == NNGP_MODEL_PARAREAL) {   // (uF - uG_prev) + uG_new, models.py:82-83
             rc = nngp_parareal_update(d, UF + (size_t)(i + 1) * d, UG + (size_t)(i + 1) * d, ug_next,
                                       u_next, stream);
-        } else {
-            const size_t j = (size_t)(i - I);
-            rc = predict_impl(X, Y, rows, d, ui, m, n_jitter, jitter_exp_host, n_restarts,
-                              theta0 + j * n_fits * 2, fatol, xatol, maxfev, preds_scratch, ug_next, u_next,
-                              nullptr, spec ? spec_idx + j * m : nullptr, spec ? spec_fits + j * n_fits * 4 : nullptr,
-                              spec ? flags + j : nullptr, st);
+            continue;
+        }
+        if (W > 0) {
+            NNGP_HIP_CHECK(hipEventRecord(rs->ev_g, st));                  // G(U1[i]) done
+            if (respec_pending) NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_r, 0));   // lists/fits ready
+            respec_pending = false;
+        }
+        rc = predict_impl(X, Y, rows, d, ui, m, n_jitter, jitter_exp_host, n_restarts, theta0 + j * n_fits * 2, fatol,
+                          xatol, maxfev, preds_scratch, ug_next, u_next, nullptr, spec ? spec_idx + j * m : nullptr,
+                          spec ? spec_fits + j * n_fits * 4 : nullptr, spec ? flags + j : nullptr,
+                          W > 0 ? spec2_idx + j * m : nullptr, W > 0 ? spec2_fits + j * n_fits * 4 : nullptr,
+                          (W > 0 && i + 1 < N) ? rs->hflags + j : nullptr, st);   // every written flag is awaited
+        if (rc || W == 0 || i + 1 >= N) continue;
+        int32_t hit = 0;
+        rc = wait_flag(rs->hflags + j, st, &hit);
+        if (rc || hit != 0) continue;
+        // miss: re-guess slices i+1 .. i+w from the actual U1[i] on the side stream
+        const int w = (int)std::min<int64_t>(W, N - 1 - i);
+        hipStream_t s2 = rs->st2;
+        double *g2 = Qr + (size_t)W * d;
+        NNGP_HIP_CHECK(hipStreamWaitEvent(s2, rs->ev_g, 0));
+        rc = nngp_parareal_update(d, UF + (size_t)(i + 1) * d, UG + (size_t)(i + 1) * d, ug_next, Qr, s2);
+        for (int q = 1; q < w && rc == NNGP_OK; q++) {
+            const int s = i + q;
+            rc = nngp_rk_batch(sys, g_tableau, g_step_mode, 1, t + s, t + s + 1, g_steps, Qr + (size_t)(q - 1) * d, g2,
+                               s2);
+            if (rc == NNGP_OK)
+                rc = nngp_parareal_update(d, UF + (size_t)(s + 1) * d, UG + (size_t)(s + 1) * d, g2,
+                                          Qr + (size_t)q * d, s2);
+        }
+        if (rc == NNGP_OK)
+            rc = spec_batch(X, Y, rows, d, Qr, w, m, n_jitter, jitter_exp_host, n_restarts,
+                            theta0 + (j + 1) * n_fits * 2, fatol, xatol, maxfev, spec2_idx + (j + 1) * m,
+                            spec2_fits + (j + 1) * n_fits * 4, true, s2);
+        if (rc == NNGP_OK) {
+            NNGP_HIP_CHECK(hipEventRecord(rs->ev_r, s2));
+            respec_pending = true;
         }
     }
+    if (respec_pending && rc == NNGP_OK) NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_r, 0));
     if (spec_hits_out && rc == NNGP_OK) {   // speculation hits (0 when not speculating)
         *spec_hits_out = 0;
         if (spec) {
             std::vector<int32_t> h((size_t)nq);
             NNGP_HIP_CHECK(hipMemcpyAsync(h.data(), flags, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, st));
             NNGP_HIP_CHECK(hipStreamSynchronize(st));
-            for (int32_t v : h) *spec_hits_out += v;
+            for (int32_t v : h) *spec_hits_out += v != 0;
         }
     }
     if (ev && rc == NNGP_OK) {   // sum the G launches once the sweep has drained

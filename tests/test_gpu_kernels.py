@@ -120,7 +120,7 @@ def test_parareal_update_kernel(gpu):
 
 
 # ---------------------------------------------------------------------------------- GP pieces
-@pytest.mark.parametrize('rows,d,m', [(640, 3, 10), (3000, 128, 15), (700, 200, 20), (33, 3, 33)])
+@pytest.mark.parametrize('rows,d,m', [(640, 3, 10), (3000, 128, 15), (700, 200, 20), (33, 3, 33), (5000, 2, 12), (1100, 128, 15)])
 def test_knn_vs_oracle(gpu, rows, d, m):
     import torch
     m = min(m, 32)

@@ -119,10 +119,13 @@ def test_burgers_n128_first_iteration_bitwise_equals_oracle(gpu):
     assert np.array_equal(np.nan_to_num(r['u'], nan=7.0), np.nan_to_num(o['u'], nan=7.0))
 
 
+@pytest.mark.parametrize('window', ['0', '4'])
 @pytest.mark.parametrize('case', ['burgers', 'lorenz'])
-def test_speculative_sweep_is_bitwise_and_hits(gpu, case):
+def test_speculative_sweep_is_bitwise_and_hits(gpu, case, window, monkeypatch):
     """The speculative sweep (every slice's fits batched up front for a Parareal-guessed query,
-    reused where the actual ordered kNN list matches) changes no bit of the run."""
+    reused where the actual ordered kNN list matches; window > 0: after a miss the next slices are
+    re-guessed from the actual state on a side stream) changes no bit of the run."""
+    monkeypatch.setenv('NNGP_RESPEC_W', window)
     if case == 'burgers':
         ode = gpu.Burgers(d_x=128, normalization='-11')
         s = gpu.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
@@ -138,5 +141,5 @@ def test_speculative_sweep_is_bitwise_and_hits(gpu, case):
     assert a['k'] == b['k'] and a['conv_int'] == b['conv_int']
     assert np.array_equal(np.nan_to_num(a['u'], nan=7.0), np.nan_to_num(b['u'], nan=7.0))
     hits = b['timings']['spec_hits']
-    print(case, 'speculation hits per iteration', hits)
+    print(case, window, 'speculation hits per iteration', hits)
     assert sum(hits) > 0 and a['timings']['spec_hits'] == [0] * len(hits)

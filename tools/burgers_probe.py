@@ -27,4 +27,4 @@ if __name__ == '__main__':
         s, r = run(es)
         tm = r['timings']
         print(f"early_stop={es}: {s:.3f} s  K={r['k']}  F={tm['F_time']:.3f} G={tm['G_time']:.3f} "
-              f"mdl={tm['mdl_tot_t']:.3f}", flush=True)
+              f"mdl={tm['mdl_tot_t']:.3f} hits={tm.get('spec_hits')}", flush=True)
