@@ -209,8 +209,51 @@ __device__ __forceinline__ void wave_key_min(uint64_t &bk, int &bi) {
     bi = ri;
 }
 
+// total order of doubles as u64 keys (NaN above everything, -0.0 == +0.0) for arg-min reductions
+__device__ __forceinline__ uint64_t fval_key(double v) {
+    if (v != v) return ~0ull;
+    if (v == 0.0) return 0x8000000000000000ull;
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+// minimum over each 16-lane row only (the 4 DPP levels of wave_key_min)
+__device__ __forceinline__ void row_key_min(uint64_t &bk, int &bi) {
+    key_min_dpp<0xB1>(bk, bi);
+    key_min_dpp<0x4E>(bk, bi);
+    key_min_dpp<0x141>(bk, bi);
+    key_min_dpp<0x140>(bk, bi);
+}
+
+// Merge 4 ascending lists of m (key, index) pairs (lists k[0..3][*], index -1 = empty slot) into
+// the m smallest in order: a wave's lane t < 4m ranks its pair against all 4m, and a valid pair
+// of rank < m lands at that position (ok[]/oi[], or as index + value into oi32/od when ok null).
+template <typename KI>
+__device__ __forceinline__ void rank_merge(const uint64_t (*k)[32], const int (*ki)[32], int m, int lane, KI *ok,
+                                           int *oi, double *od = nullptr) {
+    const int n = 4 * m;
+    for (int t = lane; t < n; t += 64) {
+        const int tl = t / m, tq = t - tl * m;
+        const uint64_t ck = k[tl][tq];
+        const int ci = ki[tl][tq];
+        if (ci < 0) continue;
+        int rank = 0;
+#pragma unroll
+        for (int L = 0; L < 4; L++)
+            for (int q = 0; q < m; q++) {
+                const int ui = ki[L][q];
+                rank += (ui >= 0) & key_less(k[L][q], ui, ck, ci);
+            }
+        if (rank < m) {
+            if (ok) ok[rank] = ck;
+            oi[rank] = ci;
+            if (od) od[rank] = __longlong_as_double((long long)ck);
+        }
+    }
+}
+
 // LDS staging of the m selected rows for the pair distances (at most 48 KB; larger m*d reads X)
-static inline int knn_xs_doubles(int m, int64_t d) { return (int64_t)m * d <= 6144 ? (int)(m * d) : 0; }
+static inline int knn_xs_doubles(int m, int64_t d) { return (int64_t)m * (d + 1) <= 6144 ? (int)(m * (d + 1)) : 0; }
 static inline size_t knn_xs_bytes(int m, int64_t d) { return (size_t)knn_xs_doubles(m, d) * sizeof(double); }
 
 template <int K> __global__ void knn_select_kernel(const double *, int64_t, int, const double *, const double *, int,
@@ -257,19 +300,22 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
     if (D2) D2 += (size_t)qy * m * m;
     if (kd2) kd2 += (size_t)qy * m;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    // 1) each wave: its m best (value, index) keys among rows wid, wid+4, ... in ascending key
-    //    order, by m rounds of "smallest key strictly after the previous pick" with a
-    //    wave-wide DPP key minimum (no block barriers)
-    __shared__ uint64_t cv[4][64];
-    __shared__ int ci[4][64];
+    // 1) each 16-lane row of the workgroup: its m best (key, index) pairs among its lanes' rows
+    //    (row r of the training set belongs to thread r % 256), in ascending order, by m rounds of
+    //    "smallest pair strictly after the previous pick" with a 4-level DPP row minimum
+    __shared__ uint64_t rk[16][32];
+    __shared__ int ri[16][32];
+    __shared__ uint64_t wk[4][32];
+    __shared__ int wi[4][32];
     {
-        // K > 0: the lane's K keys (rows lane + 64*wid + 256*j) stay in registers for all m rounds
+        const int grp = tid >> 4;
+        // K > 0: the thread's K keys (rows tid + 256*j) stay in registers for all m rounds
         uint64_t kv[K > 0 ? K : 1];
         int kr[K > 0 ? K : 1];
         if constexpr (K > 0) {
 #pragma unroll
             for (int j = 0; j < K; j++) {
-                const int r = wid * 64 + lane + 256 * j;
+                const int r = tid + 256 * j;
                 kr[j] = r < rows ? r : -1;
                 kv[j] = r < rows ? dist_key(dist[r]) : 0;
             }
@@ -281,45 +327,32 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
             int bi = -1;
             if constexpr (K > 0) {
 #pragma unroll
-                for (int j = 0; j < K; j++)   // strictly after the last pick
+                for (int j = 0; j < K; j++)
                     key_take(bk, bi, kv[j], key_less(pk, pi, kv[j], kr[j]) ? kr[j] : -1);
             } else {
-                for (int r = wid * 64 + lane; r < rows; r += 256) {
+                for (int r = tid; r < rows; r += 256) {
                     const uint64_t v = dist_key(dist[r]);
                     key_take(bk, bi, v, key_less(pk, pi, v, r) ? r : -1);
                 }
             }
-            wave_key_min(bk, bi);
-            if (lane == 0) {
-                cv[wid][k] = bk;
-                ci[wid][k] = bi;
+            row_key_min(bk, bi);
+            if ((tid & 15) == 0) {
+                rk[grp][k] = bk;
+                ri[grp][k] = bi;
             }
-            pk = bk;
-            pi = bi;
+            if (bi >= 0) {   // an exhausted row keeps its last pick (no re-picking from the start)
+                pk = bk;
+                pi = bi;
+            }
         }
     }
     __syncthreads();
-    // 2) wave 0 merges the 4 sorted candidate lists (the global m smallest keys are among them)
-    if (wid == 0) {
-        uint64_t pk = 0;
-        int pi = -1;
-        for (int k = 0; k < m; k++) {
-            uint64_t bk = 0;
-            int bi = -1;
-            for (int t2 = lane; t2 < 4 * m; t2 += 64) {
-                const uint64_t v = cv[t2 / m][t2 % m];
-                const int r = ci[t2 / m][t2 % m];
-                key_take(bk, bi, v, key_less(pk, pi, v, r) ? r : -1);
-            }
-            wave_key_min(bk, bi);
-            if (lane == 0) {
-                sel[k] = (int32_t)bi;
-                seld[k] = __longlong_as_double((long long)bk);
-            }
-            pk = bk;
-            pi = bi;
-        }
-    }
+    // 2) each wave merges its 4 row lists by rank (a pair's rank = how many valid pairs precede
+    //    it; pairs are distinct, so ranks are too), 3) wave 0 merges the 4 wave lists the same way
+    for (int t = lane; t < m; t += 64) wi[wid][t] = -1;
+    rank_merge(&rk[4 * wid], &ri[4 * wid], m, lane, wk[wid], wi[wid]);
+    __syncthreads();
+    if (wid == 0) rank_merge(wk, wi, m, lane, (uint64_t *)nullptr, sel, seld);
     __syncthreads();
     for (int k = tid; k < m; k += 256) {
         idx_out[k] = sel[k];
@@ -335,34 +368,39 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
         *hit_flag = hit;
         if (host_flag) __hip_atomic_store(host_flag, hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    if (ymT) {
+    if (ymT) {   // coalesced row reads, transposed writes
         for (int t = tid; t < m * d; t += 256) {
-            const int r = t % m, c = t / m;
+            const int r = t / d, c = t - r * d;
             ymT[c * m + r] = Y[(int64_t)sel[r] * d + c];
         }
     }
     if (D2) {
         // lower triangle incl. diagonal, mirrored ((a-b)^2 == (b-a)^2 bitwise); the m neighbour
-        // rows are staged in LDS with coalesced loads when they fit (xs_cap doubles)
+        // rows are staged in LDS with coalesced loads when they fit (xs_doubles), at a row stride
+        // of d+1 doubles so that lanes reading different rows hit different banks
         extern __shared__ __attribute__((aligned(16))) double xs[];
-        const int xs_cap = xs_doubles;
-        const bool staged = (int64_t)m * d <= xs_cap;
+        const int ds = d + 1;
+        const bool staged = (int64_t)m * ds <= xs_doubles;
         if (staged)
-            for (int t = tid; t < m * d; t += 256) xs[t] = X[(int64_t)sel[t / d] * d + t % d];
+            for (int t = tid; t < m * d; t += 256) {
+                const int r = t / d, c = t - r * d;
+                xs[r * ds + c] = X[(int64_t)sel[r] * d + c];
+            }
         __syncthreads();
         const int npairs = m * (m + 1) / 2;
         for (int t = tid; t < npairs; t += 256) {
             int r = 0;
             while ((r + 1) * (r + 2) / 2 <= t) r++;
             const int j = t - r * (r + 1) / 2;
-            const double *xr = staged ? xs + (size_t)r * d : X + (int64_t)sel[r] * d;
-            const double *xj = staged ? xs + (size_t)j * d : X + (int64_t)sel[j] * d;
+            const double *xr = staged ? xs + (size_t)r * ds : X + (int64_t)sel[r] * d;
+            const double *xj = staged ? xs + (size_t)j * ds : X + (int64_t)sel[j] * d;
             const double v = pw_sqdiff(xr, xj, d);
             D2[r * m + j] = v;
             D2[j * m + r] = v;
         }
         if (kd2)
-            for (int r = tid; r < m; r += 256) kd2[r] = pw_sqdiff(X + (int64_t)sel[r] * d, q, d);
+            for (int r = tid; r < m; r += 256)
+                kd2[r] = pw_sqdiff(staged ? xs + (size_t)r * ds : X + (int64_t)sel[r] * d, q, d);
     }
 }
 
@@ -1133,13 +1171,15 @@ __global__ void __launch_bounds__(256) gp_mean_kernel(NMArgs a) {
         const int sk = a.skip ? *a.skip : 0;
         const double *FB = sk == 0 ? a.fits_out : (sk == 2 ? a.fits_alt2 : a.fits_alt);
         const double *F = FB + (size_t)4 * cc * nfc;
-        int best = 0;
-        double bv = F[2];
-        for (int t = 1; t < nfc; t++)
-            if (F[4 * t + 2] < bv) {
-                bv = F[4 * t + 2];
-                best = t;
-            }
+        // arg-min of fval with the sequential scan's semantics (models.py:205-207 np.argmin over
+        // a scan "if f < best"): a NaN first value wins, NaNs never do later, ties keep the first.
+        // The row's lanes load the values together and reduce (key, index) pairs.
+        uint64_t bk = ~0ull;
+        int bi = -1;
+        for (int t = l; t < nfc; t += 16) key_take(bk, bi, fval_key(F[4 * t + 2]), t);
+        row_key_min(bk, bi);
+        const double f0 = F[2];
+        const int best = (f0 != f0) ? 0 : bi;
         sx = F[4 * best];
         sy = F[4 * best + 1];
         jidx = best / a.R;
