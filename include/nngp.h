@@ -180,6 +180,11 @@ int nngp_predict(const double *X, const double *Y, int64_t rows, int d, const do
  *   g_ms_out: HOST, total device time of the G launches (ms), or NULL (no timing events).    */
 #define NNGP_MODEL_PARAREAL 0
 #define NNGP_MODEL_NNGP 1
+/* NNGP_MODEL_GPFULL: the full-data GP posterior mean (GPjax_p.predict, models.py:456-462) with
+ * Y = alpha DEVICE [d][rows] and theta0 = coefficients DEVICE [d][2] = (-0.5/sigma_x^2, sigma_y^2)
+ * from nngp_gpfull_fit/nngp_gpfull_lml; m, n_jitter, jitter_exp_host, n_restarts, fatol, xatol,
+ * maxfev, preds_scratch and speculate are unused. */
+#define NNGP_MODEL_GPFULL 2
 int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps,
                           const double *t, int I, int N, double *U1, double *UG1, const double *UF,
                           const double *UG, int model, const double *X, const double *Y, int64_t rows,
@@ -187,6 +192,35 @@ int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mode
                           const double *theta0, double fatol, double xatol, int maxfev,
                           double *preds_scratch, int speculate, int32_t *spec_hits_out, float *g_ms_out,
                           void *stream);
+
+/* ---- 4. full-data GParareal (models.GPjax_p, models.py:273-473) ------------------------------
+ * The training set X, Y: DEVICE [rows][d], rows <= 7936.  K = sigma_y^2 exp(-0.5/sigma_x^2 D^2)
+ * + 10^jitter I over ALL rows (kernel_np / _fit_gp_np, models.py:300-312), theta = (sigma_x,
+ * sigma_y) in linear units.  Points and fits are batched: one blocked Cholesky per point.
+ *
+ * nngp_gpfull_lml: -LML of n_pts points (GPjax_p.log_lik, models.py:321-327; +inf when the
+ * Cholesky fails).  coord, jitter_exp, theta [n_pts][2], fval_out: HOST.  alpha_out: DEVICE
+ * [n_pts][rows] = L^-T L^-1 y (the posterior weights _predict uses, models.py:446-451) or NULL. */
+int nngp_gpfull_lml(const double *X, int64_t rows, int d, const double *Y, int n_pts,
+                    const int32_t *coord, const double *jitter_exp, const double *theta,
+                    double *fval_out, double *alpha_out, void *stream);
+
+/* nngp_gpfull_fit: n_fit Nelder-Mead fits (GPjax_p.opt_theta, models.py:329-335: scipy NM,
+ * fatol/xatol, maxiter = maxfev) of -LML for (coord[f], jitter_exp[f]) from theta0[f], all fits
+ * advancing together, one batched evaluation per round; replaces pool.map(_get_opt_par, ...)
+ * in GPjax_p._train (models.py:376-407) and _train_coord_rnd (:352-374).  All arrays HOST
+ * except X, Y.  theta_out [n_fit][2], fval_out [n_fit], nfev_out [n_fit] or NULL, rounds_out
+ * (number of evaluation rounds) or NULL. */
+int nngp_gpfull_fit(const double *X, int64_t rows, int d, const double *Y, int n_fit,
+                    const int32_t *coord, const double *jitter_exp, const double *theta0,
+                    double fatol, double xatol, int maxfev, double *theta_out, double *fval_out,
+                    int32_t *nfev_out, int32_t *rounds_out, void *stream);
+
+/* nngp_gpfull_mean: posterior means of all d coordinates at q (GPjax_p.predict -> _predict,
+ * models.py:441-462): out[j] = sum_i sigma_y^2 exp(c cdist(x_i, q)) alpha[j][i] (+ bias[j]).
+ * coef DEVICE [d][2] = (-0.5/sigma_x^2, sigma_y^2), alpha DEVICE [d][rows]; bias may be NULL. */
+int nngp_gpfull_mean(const double *X, int64_t rows, int d, const double *q, const double *coef,
+                     const double *alpha, const double *bias, double *out, void *stream);
 
 #ifdef __cplusplus
 }

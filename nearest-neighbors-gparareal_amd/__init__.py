@@ -4,7 +4,7 @@ fine RK propagator and the nearest-neighbour GP correction as hand-written HIP k
 from . import _lib, legacy
 from ._lib import NNGPError, build, lib
 from .configs import Config
-from .models import BareParareal, ModelAbstr, NNGP_p
+from .models import BareParareal, GPjax_p, ModelAbstr, NNGP_p
 from .parareal import GpuPool, MyPool, Parareal
 from .solver import SolverAbstr, SolverRK
 from .systems import (ODE, Brusselator, Burgers, DblPend, FHN_ODE, FHN_PDE, Hopf, Lorenz, Rossler,

@@ -22,8 +22,9 @@ STEP_FIXED, STEP_LINSPACE = 0, 1
 
 EXPORTS = ['nngp_abi_version', 'nngp_last_error', 'nngp_device_count', 'nngp_rk_batch', 'nngp_rk_batch_grid',
            'nngp_rhs_batch', 'nngp_parareal_update', 'nngp_knn', 'nngp_nm_fit_batch',
-           'nngp_gp_mean', 'nngp_predict', 'nngp_correction_sweep']
-MODEL_PARAREAL, MODEL_NNGP = 0, 1
+           'nngp_gp_mean', 'nngp_predict', 'nngp_correction_sweep', 'nngp_gpfull_lml', 'nngp_gpfull_fit',
+           'nngp_gpfull_mean']
+MODEL_PARAREAL, MODEL_NNGP, MODEL_GPFULL = 0, 1, 2
 
 
 class NNGPError(RuntimeError):
@@ -74,6 +75,10 @@ def lib():
     L.nngp_correction_sweep.argtypes = [ctypes.POINTER(CSystem), i32, i32, i64, _vp, i32, i32, _vp, _vp, _vp,
                                         _vp, i32, _vp, _vp, i64, i32, i32, _dp, i32, _vp, dbl, dbl, i32,
                                         _vp, i32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_float), _vp]
+    _ip = ctypes.POINTER(ctypes.c_int32)
+    L.nngp_gpfull_lml.argtypes = [_vp, i64, i32, _vp, i32, _ip, _dp, _dp, _dp, _vp, _vp]
+    L.nngp_gpfull_fit.argtypes = [_vp, i64, i32, _vp, i32, _ip, _dp, _dp, dbl, dbl, i32, _dp, _dp, _ip, _ip, _vp]
+    L.nngp_gpfull_mean.argtypes = [_vp, i64, i32, _vp, _vp, _vp, _vp, _vp, _vp]
     for name in EXPORTS:
         if name not in ('nngp_abi_version', 'nngp_last_error', 'nngp_device_count'):
             getattr(L, name).restype = i32

@@ -48,7 +48,7 @@ void set_error(const char *fmt, ...);
 // speculative sweep's batch buffers, which must outlive the per-slice calls.  Growing a slot
 // frees the old buffer after hipFree's implicit device synchronisation.  Not thread-safe across
 // host threads sharing a device.
-constexpr int N_WS_SLOTS = 3;   // slot 2: the sweep's speculation buffers
+constexpr int N_WS_SLOTS = 4;   // slot 2: the sweep's speculation buffers; slot 3: full-GP factors
 void *workspace(size_t bytes, int *err, int slot = 0);
 
 int predict_impl(const double *X, const double *Y, int64_t rows, int d, const double *new_x, int m,
@@ -57,6 +57,8 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
                  double *out, double *fits_out, const int32_t *spec_idx, const double *spec_fits,
                  int32_t *hit_flag, const int32_t *spec2_idx, const double *spec2_fits, int32_t *host_flag,
                  hipStream_t st);
+int gpfull_mean(const double *X, int64_t rows, int d, const double *q, const double *coef, const double *alpha,
+                const double *bias, double *out, hipStream_t st);
 int spec_batch(const double *X, const double *Y, int64_t rows, int d, const double *Q, int nq, int m,
                int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
                double fatol, double xatol, int maxfev, int32_t *idx_out, double *fits_out, bool latency,

@@ -1,0 +1,472 @@
+// nngp_gpfull.hip -- full-data GParareal correction (models.GPjax_p, models.py:273-473) on gfx950.
+//
+// The reference fits, per coordinate j and jitter in arange(-20, -11), the squared-exponential GP
+// of ALL training rows (rows ~ N*K, hundreds to thousands) by Nelder-Mead on theta = (sigma_x,
+// sigma_y) warm-started at the previous iteration's optimum (models.py:376-407 -> opt_theta
+// :329-335 -> log_lik :321-327 -> _log_lik_np :314-319 -> _fit_gp_np :306-312):
+//     K     = sigma_y^2 * exp(-0.5 * (1/sigma_x^2) * cdist(x, x, 'sqeuclidean')) + 10^jitter I
+//     L     = cholesky(K)                 (LinAlgError -> +inf)
+//     alpha = L^-T (L^-1 y)
+//     -LML  = -(-0.5 y.alpha - sum(log diag L) - (rows/2) log 2 pi)
+// Every Nelder-Mead round evaluates one point per unfinished fit; all of them form ONE batch of
+// rows x rows factorisations here:
+//   gpf_build_kernel   K of every point of the batch (lower triangle), from the hoisted D^2
+//   gpf_panel_kernel   blocked right-looking Cholesky, panel j: factor the 32x32 diagonal block
+//                      in LDS, solve the rows below against it (one row per thread)
+//   gpf_syrk_kernel    trailing update A22 -= L21 L21^T, 32x32 lower tiles, LDS-staged panels
+//   gpf_solve_kernel   forward / back substitution (32-row blocks: a wave solves the block in
+//                      registers, the workgroup updates the rest) and the -LML reduction
+// FP64 VALU is the MI355X's FP64 peak (the FP64 MFMA rate is the same), so the tiles use plain
+// VALU FMAs.  The arithmetic order of LAPACK's blocked potrf is not reproduced (it is
+// third-party and build-dependent); parity is to tolerance (tests/test_gpu_gpfull.py).
+// The Nelder-Mead state machines (nngp_nm.h, scipy's semantics) run on the host, one per fit.
+#include <cmath>
+#include <vector>
+
+#include "common.h"
+#include "nngp_nm.h"
+
+namespace nngp {
+
+static constexpr int GPB = 32;                       // panel width
+static constexpr double GPF_LOG_2PI = 1.8378770664093453;   // np.log(2*np.pi)
+static constexpr int GPF_MAX_ROWS = 7936;            // the solve vector lives in LDS (<= 62 KB)
+
+__device__ __forceinline__ void wave_sync_lds() {   // order one wave's LDS writes before its reads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct GPPoint {      // one evaluation: kernel coefficients and the training column
+    double c;         // -0.5 * (1 / sigma_x^2)
+    double psy;       // sigma_y^2
+    double jp;        // 10^jitter
+    int coord;        // column of Y
+    int pad;
+};
+
+// D2 = cdist(x, x, 'sqeuclidean'): sequential sum over the d components (scipy's loop)
+__global__ void gpf_d2_kernel(const double *__restrict__ X, int n, int d, double *__restrict__ D2) {
+    const int j = blockIdx.x * 16 + threadIdx.x, i = blockIdx.y * 16 + threadIdx.y;
+    if (i >= n || j >= n) return;
+    double acc = 0.0;
+    for (int c = 0; c < d; c++) {
+        const double t = X[(size_t)i * d + c] - X[(size_t)j * d + c];
+        acc = acc + t * t;
+    }
+    D2[(size_t)i * n + j] = acc;
+}
+
+// lower triangle (incl. diagonal) of K for point b: sigma_y^2 * exp(c * D2) (+ 10^jitter on the
+// diagonal), kernel_np's order (models.py:302-304) and K + eye*10**jitter (:308)
+__global__ void gpf_build_kernel(const double *__restrict__ D2, int n, const GPPoint *__restrict__ pts,
+                                 double *__restrict__ A, const int32_t *__restrict__ fail) {
+    const int b = blockIdx.y;
+    if (fail[b]) return;
+    const GPPoint p = pts[b];
+    double *Ab = A + (size_t)b * n * n;
+    const size_t nn = (size_t)n * n;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < nn; t += (size_t)gridDim.x * blockDim.x) {
+        const int i = (int)(t / n), j = (int)(t - (size_t)i * n);
+        if (j > i) continue;
+        double v = p.psy * exp(p.c * D2[t]);
+        if (i == j) v = v + p.jp;
+        Ab[t] = v;
+    }
+}
+
+// Panel p0 (width pb), one workgroup per matrix: wave 0 factors the diagonal block in LDS (one
+// wave: no block barrier inside the column loop), the block is written back, and each thread
+// solves rows below it: L21[r,:] = A21[r,:] L11^-T.  A pivot that is not > 0 (or NaN) is
+// LAPACK's info > 0: the point fails (+inf).
+__global__ void __launch_bounds__(256) gpf_panel_kernel(double *__restrict__ A, int n, int p0, int pb,
+                                                         int32_t *__restrict__ fail) {
+    const int b = blockIdx.y;
+    if (fail[b]) return;
+    double *Ab = A + (size_t)b * n * n;
+    __shared__ double L[GPB][GPB + 1];
+    __shared__ int bad;
+    const int tid = threadIdx.x;
+    for (int t = tid; t < GPB * GPB; t += 256) {
+        const int i = t / GPB, j = t % GPB;
+        L[i][j] = (i < pb && j <= i) ? Ab[(size_t)(p0 + i) * n + p0 + j] : 0.0;
+    }
+    if (tid == 0) bad = 0;
+    __syncthreads();
+    if (tid < 64) {
+        const int i = tid;   // lane i owns row i of the block
+        for (int j = 0; j < pb; j++) {
+            const double djj = L[j][j];
+            if (!(djj > 0.0)) {   // uniform: every lane read the same value
+                if (i == 0) bad = 1;
+                break;
+            }
+            const double ljj = sqrt(djj);
+            if (i == j) L[j][j] = ljj;
+            if (i > j && i < pb) L[i][j] = L[i][j] / ljj;
+            wave_sync_lds();
+            if (i > j && i < pb) {
+                const double lij = L[i][j];
+                for (int k = j + 1; k <= i; k++) L[i][k] = L[i][k] - lij * L[k][j];
+            }
+            wave_sync_lds();
+        }
+    }
+    __syncthreads();
+    if (bad) {
+        if (tid == 0) fail[b] = 1;
+        return;
+    }
+    for (int t = tid; t < pb * pb; t += 256) {
+        const int i = t / pb, j = t % pb;
+        if (j <= i) Ab[(size_t)(p0 + i) * n + p0 + j] = L[i][j];
+    }
+    for (int r = p0 + pb + tid; r < n; r += 256) {
+        double x[GPB];
+        double *row = Ab + (size_t)r * n + p0;
+#pragma unroll
+        for (int k = 0; k < GPB; k++) x[k] = k < pb ? row[k] : 0.0;
+#pragma unroll
+        for (int j = 0; j < GPB; j++) {
+            if (j < pb) {
+                double s = x[j];
+#pragma unroll
+                for (int k = 0; k < GPB; k++)
+                    if (k < j) s = s - x[k] * L[j][k];
+                x[j] = s / L[j][j];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < GPB; k++)
+            if (k < pb) row[k] = x[k];
+    }
+}
+
+// trailing update of the lower triangle below panel p0: A[i][j] -= sum_k L[i][p0+k] L[j][p0+k],
+// i >= j >= q0 = p0 + pb; workgroup = one 32x32 tile (ti >= tj), thread = 2x2 outputs
+__global__ void __launch_bounds__(256) gpf_syrk_kernel(double *__restrict__ A, int n, int p0, int pb,
+                                                        const int32_t *__restrict__ fail) {
+    const int b = blockIdx.y;
+    if (fail[b]) return;
+    double *Ab = A + (size_t)b * n * n;
+    const int q0 = p0 + pb;
+    // blockIdx.x -> (ti, tj), ti >= tj, row-major over the lower triangle of tiles
+    int ti = (int)((sqrt(8.0 * blockIdx.x + 1.0) - 1.0) / 2.0);
+    while ((ti + 1) * (ti + 2) / 2 <= (int)blockIdx.x) ti++;
+    while (ti * (ti + 1) / 2 > (int)blockIdx.x) ti--;
+    const int tj = blockIdx.x - ti * (ti + 1) / 2;
+    const int i0 = q0 + ti * 32, j0 = q0 + tj * 32;
+    __shared__ double Li[32][GPB + 1], Lj[32][GPB + 1];
+    const int tid = threadIdx.x;
+    for (int t = tid; t < 32 * GPB; t += 256) {
+        const int r = t / GPB, k = t % GPB;
+        Li[r][k] = (i0 + r < n && k < pb) ? Ab[(size_t)(i0 + r) * n + p0 + k] : 0.0;
+        Lj[r][k] = (j0 + r < n && k < pb) ? Ab[(size_t)(j0 + r) * n + p0 + k] : 0.0;
+    }
+    __syncthreads();
+    const int ri = (tid / 16) * 2, rj = (tid % 16) * 2;
+    double acc[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+    for (int k = 0; k < pb; k++) {
+        const double a0 = Li[ri][k], a1 = Li[ri + 1][k], b0 = Lj[rj][k], b1 = Lj[rj + 1][k];
+        acc[0][0] = acc[0][0] + a0 * b0;
+        acc[0][1] = acc[0][1] + a0 * b1;
+        acc[1][0] = acc[1][0] + a1 * b0;
+        acc[1][1] = acc[1][1] + a1 * b1;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; u++)
+#pragma unroll
+        for (int v = 0; v < 2; v++) {
+            const int i = i0 + ri + u, j = j0 + rj + v;
+            if (i < n && j <= i) Ab[(size_t)i * n + j] = Ab[(size_t)i * n + j] - acc[u][v];
+        }
+}
+
+__device__ __forceinline__ double block_sum(double v, double *red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); w++) s = s + red[w];
+    __syncthreads();
+    return s;
+}
+
+// forward z = L^-1 y, back alpha = L^-T z (solve_triangular twice, models.py:311), then
+// -LML = -(-0.5 * y.alpha - sum(log diag L) - (n/2) log 2pi) (:318); +inf on failure/NaN
+__global__ void __launch_bounds__(256) gpf_solve_kernel(const double *__restrict__ A, int n,
+                                                         const double *__restrict__ Y, int d,
+                                                         const GPPoint *__restrict__ pts,
+                                                         const int32_t *__restrict__ fail,
+                                                         double *__restrict__ fval, double *__restrict__ alpha_out) {
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (fail[b]) {
+        if (tid == 0) fval[b] = INFINITY;
+        return;
+    }
+    const double *Ab = A + (size_t)b * n * n;
+    const int coord = pts[b].coord;
+    extern __shared__ double r[];   // [n]
+    __shared__ double red[4];
+    for (int i = tid; i < n; i += 256) r[i] = Y[(size_t)i * d + coord];
+    __syncthreads();
+    // forward substitution, 32-row blocks top-down
+    for (int p0 = 0; p0 < n; p0 += GPB) {
+        const int pb = min(GPB, n - p0);
+        if (tid < 64) {
+            double v = lane < pb ? r[p0 + lane] : 0.0;
+            for (int j = 0; j < pb; j++) {
+                const double zj = __shfl(v, j, 64) / Ab[(size_t)(p0 + j) * n + p0 + j];
+                if (lane == j) v = zj;
+                if (lane > j && lane < pb) v = v - Ab[(size_t)(p0 + lane) * n + p0 + j] * zj;
+            }
+            if (lane < pb) r[p0 + lane] = v;
+        }
+        __syncthreads();
+        for (int i = p0 + pb + tid; i < n; i += 256) {
+            double s = r[i];
+            const double *Li = Ab + (size_t)i * n + p0;
+            for (int k = 0; k < pb; k++) s = s - Li[k] * r[p0 + k];
+            r[i] = s;
+        }
+        __syncthreads();
+    }
+    // back substitution with L^T, 32-row blocks bottom-up
+    const int nblk = (n + GPB - 1) / GPB;
+    for (int bk = nblk - 1; bk >= 0; bk--) {
+        const int p0 = bk * GPB, pb = min(GPB, n - p0);
+        if (tid < 64) {
+            double v = lane < pb ? r[p0 + lane] : 0.0;
+            for (int j = pb - 1; j >= 0; j--) {
+                const double aj = __shfl(v, j, 64) / Ab[(size_t)(p0 + j) * n + p0 + j];
+                if (lane == j) v = aj;
+                if (lane < j) v = v - Ab[(size_t)(p0 + j) * n + p0 + lane] * aj;
+            }
+            if (lane < pb) r[p0 + lane] = v;
+        }
+        __syncthreads();
+        for (int i = tid; i < p0; i += 256) {   // rows above: r_i -= sum_k L[p0+k][i] alpha_k
+            double s = r[i];
+            for (int k = 0; k < pb; k++) s = s - Ab[(size_t)(p0 + k) * n + i] * r[p0 + k];
+            r[i] = s;
+        }
+        __syncthreads();
+    }
+    double ya = 0.0, lg = 0.0;
+    for (int i = tid; i < n; i += 256) {
+        ya = ya + Y[(size_t)i * d + coord] * r[i];
+        lg = lg + log(Ab[(size_t)i * n + i]);
+        if (alpha_out) alpha_out[(size_t)b * n + i] = r[i];
+    }
+    const double ydot = block_sum(ya, red);
+    const double slog = block_sum(lg, red);
+    if (tid == 0) {
+        const double res = -(((-0.5 * ydot) - slog) - ((double)n / 2) * GPF_LOG_2PI);
+        fval[b] = (res != res) ? INFINITY : res;
+    }
+}
+
+// posterior mean of every coordinate j at one query q (models.py:456-462 -> _predict :441-453):
+// K_star = sigma_y^2 exp(c * cdist(x, q)); mean = K_star . alpha_j; out[j] = mean + bias[j]
+__global__ void __launch_bounds__(256) gpf_mean_kernel(const double *__restrict__ X, int n, int d,
+                                                        const double *__restrict__ q,
+                                                        const double *__restrict__ coef,
+                                                        const double *__restrict__ alpha,
+                                                        const double *__restrict__ bias, double *__restrict__ out) {
+    __shared__ double red[4];
+    const int j = blockIdx.x;
+    const double c = coef[2 * j], psy = coef[2 * j + 1];
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        double dist = 0.0;
+        for (int k = 0; k < d; k++) {
+            const double t = X[(size_t)i * d + k] - q[k];
+            dist = dist + t * t;
+        }
+        acc = acc + (psy * exp(c * dist)) * alpha[(size_t)j * n + i];
+    }
+    const double mean = block_sum(acc, red);
+    if (threadIdx.x == 0) out[j] = bias ? mean + bias[j] : mean;
+}
+
+int gpfull_mean(const double *X, int64_t rows, int d, const double *q, const double *coef, const double *alpha,
+                const double *bias, double *out, hipStream_t st) {
+    hipLaunchKernelGGL(gpf_mean_kernel, dim3(d), dim3(256), 0, st, X, (int)rows, d, q, coef, alpha, bias, out);
+    NNGP_LAUNCH_CHECK();
+    return NNGP_OK;
+}
+
+// The batched -LML pipeline for nb points (device pts), D2 [n][n] given; A: nb*n*n scratch.
+static int gpf_eval(const double *D2, int n, const double *Y, int d, const GPPoint *pts, int nb, double *A,
+                    int32_t *fail, double *fval, double *alpha_out, hipStream_t st) {
+    NNGP_HIP_CHECK(hipMemsetAsync(fail, 0, sizeof(int32_t) * nb, st));
+    const size_t nn = (size_t)n * n;
+    const unsigned bx = (unsigned)std::min<size_t>((nn + 255) / 256, 1024);
+    hipLaunchKernelGGL(gpf_build_kernel, dim3(bx, nb), dim3(256), 0, st, D2, n, pts, A, fail);
+    NNGP_LAUNCH_CHECK();
+    for (int p0 = 0; p0 < n; p0 += GPB) {
+        const int pb = std::min(GPB, n - p0);
+        const int below = n - p0 - pb;
+        hipLaunchKernelGGL(gpf_panel_kernel, dim3(1, nb), dim3(256), 0, st, A, n, p0, pb, fail);
+        NNGP_LAUNCH_CHECK();
+        if (below > 0) {
+            const int nt = (below + 31) / 32;
+            hipLaunchKernelGGL(gpf_syrk_kernel, dim3((unsigned)(nt * (nt + 1) / 2), nb), dim3(256), 0, st, A, n, p0,
+                               pb, fail);
+            NNGP_LAUNCH_CHECK();
+        }
+    }
+    hipLaunchKernelGGL(gpf_solve_kernel, dim3(nb), dim3(256), sizeof(double) * n, st, A, n, Y, d, pts, fail, fval,
+                       alpha_out);
+    NNGP_LAUNCH_CHECK();
+    return NNGP_OK;
+}
+
+static GPPoint gp_point(double sx, double sy, double jexp, int coord) {
+    GPPoint p;
+    p.c = -0.5 * (1 / (sx * sx));   // -0.5 * (1/(sigma_x**2))
+    p.psy = sy * sy;                // sigma_y**2
+    p.jp = pow(10.0, jexp);         // 10**jitter
+    p.coord = coord;
+    p.pad = 0;
+    return p;
+}
+
+struct GPFWork {   // device buffers of one call
+    double *D2, *A, *fval;
+    GPPoint *pts;
+    int32_t *fail;
+};
+
+static int gpf_workspace(int n, int nb, GPFWork &w) {
+    int err = 0;
+    const size_t nn = (size_t)n * n;
+    const size_t bytes = sizeof(double) * (nn + (size_t)nb * nn + nb) + sizeof(GPPoint) * nb + sizeof(int32_t) * nb + 64;
+    char *p = (char *)workspace(bytes, &err, 3);
+    if (err) return err;
+    w.D2 = (double *)p;
+    w.A = w.D2 + nn;
+    w.fval = w.A + (size_t)nb * nn;
+    w.pts = (GPPoint *)(w.fval + nb);
+    w.fail = (int32_t *)(w.pts + nb);
+    return NNGP_OK;
+}
+
+static int gpf_check(int64_t rows, int d, int n_fit) {
+    NNGP_REQUIRE(rows >= 1 && rows <= GPF_MAX_ROWS, "full GP needs 1 <= rows <= %d (got %lld)", GPF_MAX_ROWS,
+                 (long long)rows);
+    NNGP_REQUIRE(d >= 1 && n_fit >= 1, "bad d / fit count");
+    return NNGP_OK;
+}
+
+// points per batch: all fits, capped so the factor scratch stays under ~8 GB
+static int gpf_batch_cap(int n, int n_fit) {
+    const size_t per = sizeof(double) * (size_t)n * n;
+    const size_t cap = std::max<size_t>(1, ((size_t)8 << 30) / per);
+    return (int)std::min<size_t>(cap, (size_t)n_fit);
+}
+
+}  // namespace nngp
+
+using namespace nngp;
+
+extern "C" int nngp_gpfull_lml(const double *X, int64_t rows, int d, const double *Y, int n_pts,
+                               const int32_t *coord, const double *jitter_exp, const double *theta,
+                               double *fval_out, double *alpha_out, void *stream) {
+    NNGP_REQUIRE(X && Y && coord && jitter_exp && theta && fval_out, "null argument");
+    int rc = gpf_check(rows, d, n_pts);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const int n = (int)rows, nbc = gpf_batch_cap(n, n_pts);
+    GPFWork w;
+    rc = gpf_workspace(n, nbc, w);
+    if (rc) return rc;
+    hipLaunchKernelGGL(gpf_d2_kernel, dim3((n + 15) / 16, (n + 15) / 16), dim3(16, 16), 0, st, X, n, d, w.D2);
+    NNGP_LAUNCH_CHECK();
+    std::vector<GPPoint> hp((size_t)n_pts);
+    for (int i = 0; i < n_pts; i++) {
+        NNGP_REQUIRE(coord[i] >= 0 && coord[i] < d, "coordinate %d out of range", coord[i]);
+        hp[i] = gp_point(theta[2 * i], theta[2 * i + 1], jitter_exp[i], coord[i]);
+    }
+    std::vector<double> hf((size_t)n_pts);
+    for (int s = 0; s < n_pts; s += nbc) {
+        const int nb = std::min(nbc, n_pts - s);
+        NNGP_HIP_CHECK(hipMemcpyAsync(w.pts, hp.data() + s, sizeof(GPPoint) * nb, hipMemcpyHostToDevice, st));
+        rc = gpf_eval(w.D2, n, Y, d, w.pts, nb, w.A, w.fail, w.fval, alpha_out ? alpha_out + (size_t)s * n : nullptr,
+                      st);
+        if (rc) return rc;
+        NNGP_HIP_CHECK(hipMemcpyAsync(hf.data() + s, w.fval, sizeof(double) * nb, hipMemcpyDeviceToHost, st));
+    }
+    NNGP_HIP_CHECK(hipStreamSynchronize(st));
+    for (int i = 0; i < n_pts; i++) fval_out[i] = hf[i];
+    return NNGP_OK;
+}
+
+extern "C" int nngp_gpfull_fit(const double *X, int64_t rows, int d, const double *Y, int n_fit,
+                               const int32_t *coord, const double *jitter_exp, const double *theta0,
+                               double fatol, double xatol, int maxfev, double *theta_out, double *fval_out,
+                               int32_t *nfev_out, int32_t *rounds_out, void *stream) {
+    NNGP_REQUIRE(X && Y && coord && jitter_exp && theta0 && theta_out && fval_out, "null argument");
+    int rc = gpf_check(rows, d, n_fit);
+    if (rc) return rc;
+    NNGP_REQUIRE(maxfev >= 1, "maxfev must be >= 1");
+    hipStream_t st = (hipStream_t)stream;
+    const int n = (int)rows, nbc = gpf_batch_cap(n, n_fit);
+    GPFWork w;
+    rc = gpf_workspace(n, nbc, w);
+    if (rc) return rc;
+    hipLaunchKernelGGL(gpf_d2_kernel, dim3((n + 15) / 16, (n + 15) / 16), dim3(16, 16), 0, st, X, n, d, w.D2);
+    NNGP_LAUNCH_CHECK();
+    const NMCfg cfg{fatol, xatol, maxfev, maxfev};   // maxiter = maxfev = 200*N (scipy defaults)
+    std::vector<NM> S((size_t)n_fit);
+    for (int f = 0; f < n_fit; f++) {
+        NNGP_REQUIRE(coord[f] >= 0 && coord[f] < d, "coordinate %d out of range", coord[f]);
+        S[f].f0 = S[f].f1 = S[f].f2 = INFINITY;
+        S[f].xbx = S[f].xby = S[f].xrx = S[f].xry = S[f].fxr = 0.0;
+        nm_start(S[f], cfg, theta0[2 * f], theta0[2 * f + 1]);
+    }
+    std::vector<GPPoint> hp;
+    std::vector<int> who;
+    std::vector<double> hf;
+    int rounds = 0;
+    for (;;) {
+        hp.clear();
+        who.clear();
+        for (int f = 0; f < n_fit; f++)
+            if (S[f].st != ST_DONE) {
+                hp.push_back(gp_point(S[f].px, S[f].py, jitter_exp[f], coord[f]));
+                who.push_back(f);
+            }
+        if (hp.empty()) break;
+        rounds++;
+        const int np = (int)hp.size();
+        hf.resize((size_t)np);
+        for (int s = 0; s < np; s += nbc) {
+            const int nb = std::min(nbc, np - s);
+            NNGP_HIP_CHECK(hipMemcpyAsync(w.pts, hp.data() + s, sizeof(GPPoint) * nb, hipMemcpyHostToDevice, st));
+            rc = gpf_eval(w.D2, n, Y, d, w.pts, nb, w.A, w.fail, w.fval, nullptr, st);
+            if (rc) return rc;
+            NNGP_HIP_CHECK(hipMemcpyAsync(hf.data() + s, w.fval, sizeof(double) * nb, hipMemcpyDeviceToHost, st));
+        }
+        NNGP_HIP_CHECK(hipStreamSynchronize(st));
+        for (int q = 0; q < np; q++) nm_consume(S[who[q]], cfg, hf[q]);
+    }
+    for (int f = 0; f < n_fit; f++) {
+        theta_out[2 * f] = S[f].s0x;
+        theta_out[2 * f + 1] = S[f].s0y;
+        fval_out[f] = S[f].f0;
+        if (nfev_out) nfev_out[f] = S[f].fcalls;
+    }
+    if (rounds_out) *rounds_out = rounds;
+    return NNGP_OK;
+}
+
+extern "C" int nngp_gpfull_mean(const double *X, int64_t rows, int d, const double *q, const double *coef,
+                                const double *alpha, const double *bias, double *out, void *stream) {
+    NNGP_REQUIRE(X && q && coef && alpha && out, "null argument");
+    NNGP_REQUIRE(rows >= 1 && d >= 1, "bad rows / d");
+    return gpfull_mean(X, rows, d, q, coef, alpha, bias, out, (hipStream_t)stream);
+}

@@ -126,12 +126,15 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
     using namespace nngp;
     NNGP_REQUIRE(sys != nullptr && t && U1 && UG1, "null argument");
     NNGP_REQUIRE(0 <= I && I <= N, "need 0 <= I <= N (I=%d N=%d)", I, N);
-    NNGP_REQUIRE(model == NNGP_MODEL_PARAREAL || model == NNGP_MODEL_NNGP, "unknown model %d", model);
+    NNGP_REQUIRE(model == NNGP_MODEL_PARAREAL || model == NNGP_MODEL_NNGP || model == NNGP_MODEL_GPFULL,
+                 "unknown model %d", model);
     const int d = sys->d;
     hipStream_t st = (hipStream_t)stream;
     if (model == NNGP_MODEL_PARAREAL) NNGP_REQUIRE(UF && UG, "parareal model needs UF and UG");
     if (model == NNGP_MODEL_NNGP)
         NNGP_REQUIRE(X && Y && theta0 && preds_scratch && rows >= m && m >= 1, "nngp model arguments");
+    if (model == NNGP_MODEL_GPFULL)
+        NNGP_REQUIRE(X && Y && theta0 && rows >= 1, "full-GP model arguments (X, alpha, coefficients)");
     const int64_t n_fits = (int64_t)d * n_jitter * n_restarts;
     hipEvent_t *ev = nullptr;
     if (g_ms_out) {
@@ -211,6 +214,10 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
         if (model == NNGP_MODEL_PARAREAL) {   // (uF - uG_prev) + uG_new, models.py:82-83
             rc = nngp_parareal_update(d, UF + (size_t)(i + 1) * d, UG + (size_t)(i + 1) * d, ug_next,
                                       u_next, stream);
+            continue;
+        }
+        if (model == NNGP_MODEL_GPFULL) {     // GPjax_p.predict + uG (models.py:456-462)
+            rc = gpfull_mean(X, rows, d, ui, theta0, Y, ug_next, u_next, st);
             continue;
         }
         if (W > 0) {

@@ -13,6 +13,11 @@ Compute paths (all HIP, no CPU fallback):
   predict_device(...)  device tensors, used by the Parareal driver's sequential loop
   get_preds(...)       reference signature on pre-selected (xm, ym) -> nngp_nm_fit_batch +
                        first-argmin + nngp_gp_mean (the unfused path of the same kernels)
+
+GPjax_p (models.py:273-473) is the full-data GParareal model: per coordinate and jitter a
+Nelder-Mead fit of the GP over ALL training rows, warm-started at the previous optimum, batched
+across fits on the GPU (nngp_gpfull_fit), and posterior means from the memoised Cholesky weights
+(nngp_gpfull_mean / the native sweep).
 """
 import copy
 import ctypes
@@ -270,3 +275,201 @@ class NNGP_p(ModelAbstr):
 
     def restore_attrs(self, pool):
         self.pool = pool
+
+
+def _select_fit(theta, fval, jitter):
+    """The per-coordinate choice of models.py:388-395 / 361-365: keep fits with
+    fval < 0.9 * min(fval) (all if none), then the first minimum in order (Python min, '<')."""
+    fmin = np.min(fval)
+    mask = fval < fmin * 0.9
+    if mask.sum() == 0:
+        mask[:] = True
+    idx = np.nonzero(mask)[0]
+    best = idx[0]
+    for i in idx[1:]:
+        if fval[i] < fval[best]:
+            best = i
+    return tuple(float(v) for v in theta[best]), float(fval[best]), float(jitter[best])
+
+
+class GPjax_p(ModelAbstr):
+    """Full-data GParareal correction (models.py:273-473) on the GPU.
+
+    Same constructor, attributes (thetas, jitters, hyp, fatol/xatol default 1e-4, rng =
+    default_rng(45) for the random-restart fallback) and training semantics as the reference;
+    the d*9 Nelder-Mead fits of a training round advance together, one batched rows x rows
+    factorisation per round (nngp_gpfull_fit).  The -LML arithmetic follows the reference's
+    expressions, but the Cholesky's summation order is the GPU's own (LAPACK's blocked order is
+    not reproduced): parity is to tolerance and on K (tests/test_gpu_gpfull.py)."""
+
+    def __init__(self, n, N, worker_pool=None, theta=None, jitter=None, fatol=None, xatol=None, **kwargs):
+        super().__init__(N=N, **kwargs)
+        if theta is None:
+            theta = [1, 1]
+        theta = np.array(theta)
+        self.name = 'GP'
+        self.hyp = np.ones((n, theta.shape[0], N))
+        self.thetas = [tuple(float(v) for v in theta) for _ in range(n)]
+        self.jitters = [None for _ in range(n)]
+        self.fatol = 1e-4 if fatol is None else fatol
+        self.xatol = 1e-4 if xatol is None else xatol
+        self.theta = theta
+        self.N = N
+        self.n = n
+        self.pool = worker_pool
+        self.rng = np.random.default_rng(45)
+        self.maxfev = 200 * theta.shape[0]
+        self.tot_train_t = np.zeros(N)
+        self.train_count = np.zeros(N)
+        self.k = 0
+        self.rounds = []
+        self._dev = None   # (X [rows][n], alpha [n][rows], coef [n][2]) device tensors
+
+    def get_times(self):
+        out = super().get_times()
+        with np.errstate(invalid='ignore', divide='ignore'):
+            avg = (self.tot_train_t / self.train_count)[:self.k + 1]
+        out.update({'serial_train_time': self.tot_train_t[:self.k + 1], 'avg_serial_train_time': avg})
+        return out
+
+    # ---------------------------------------------------------------------------- training
+    def _fit_batch(self, X, Y, coords, jitters, theta0):
+        """pool.map(_get_opt_par[_rnd], ...) (models.py:404-407, 355-358) as one native call."""
+        import torch
+        nf = len(coords)
+        c = np.ascontiguousarray(coords, dtype=np.int32)
+        jx, jp = _lib.host_doubles(jitters)
+        t0, tp = _lib.host_doubles(np.asarray(theta0, dtype=float).reshape(nf, 2))
+        th = np.empty((nf, 2))
+        fv = np.empty(nf)
+        ne = np.empty(nf, dtype=np.int32)
+        rounds = ctypes.c_int32(0)
+        ip = ctypes.POINTER(ctypes.c_int32)
+        st = time.time()
+        _lib.check(_lib.lib().nngp_gpfull_fit(
+            X.data_ptr(), X.shape[0], self.n, Y.data_ptr(), nf, c.ctypes.data_as(ip), jp, tp, float(self.fatol),
+            float(self.xatol), self.maxfev, th.ctypes.data_as(_lib._dp), fv.ctypes.data_as(_lib._dp),
+            ne.ctypes.data_as(ip), ctypes.byref(rounds), torch.cuda.current_stream().cuda_stream))
+        self.tot_train_t[min(self.k, self.N - 1)] += time.time() - st
+        self.train_count[min(self.k, self.N - 1)] += nf
+        self.rounds.append(int(rounds.value))
+        return th, fv, ne
+
+    def _train_coord_rnd(self, X, Y, coord):
+        """models.py:352-374: random restarts for a coordinate whose fits all failed."""
+        tot_rnd = max(3, int(self.N / 9))
+        ins = list(product([coord for _ in range(tot_rnd)], JITTERS))
+        thetas = [10 ** self.rng.uniform(-4, 1, (len(self.theta))) for _ in range(len(ins))]
+        th, fv, _ = self._fit_batch(X, Y, [i[0] for i in ins], [i[1] for i in ins], thetas)
+        opt_params, opt_fval, opt_jitter = _select_fit(th, fv, np.array([i[1] for i in ins]))
+        if np.isinf(opt_fval):
+            print('random restart failed')
+            opt_params, opt_fval, opt_jitter = self._train_coord_rnd(X, Y, coord)
+        return opt_params, opt_fval, opt_jitter
+
+    def _train(self, X, Y, old_thetas):
+        """models.py:376-417: every (coordinate, jitter) fit from the coordinate's old theta."""
+        ins = list(product(range(self.n), JITTERS))
+        th, fv, _ = self._fit_batch(X, Y, [i[0] for i in ins], [i[1] for i in ins],
+                                    [old_thetas[i[0]] for i in ins])
+        temp = np.zeros((self.n, len(self.theta)))
+        nj = len(JITTERS)
+        for j in range(self.n):
+            sl = slice(j * nj, (j + 1) * nj)
+            opt_params, opt_fval, opt_jitter = _select_fit(th[sl], fv[sl], JITTERS)
+            if np.isinf(opt_fval):
+                print('------> GP trainign failed for coordinate', j)
+                opt_params, opt_fval, opt_jitter = self._train_coord_rnd(X, Y, j)
+            self.thetas[j] = opt_params
+            self.jitters[j] = opt_jitter
+            temp[j, :] = opt_params
+        return temp
+
+    def _weights(self, X, Y):
+        """The posterior weights _predict memoises (models.py:441-453): alpha_j = K_j^-1 y_j for
+        the chosen (theta_j, jitter_j).  The reference keys its memo by theta alone, so a
+        coordinate whose theta equals an earlier coordinate's reuses that coordinate's weights
+        (reproduced)."""
+        import torch
+        n, rows = self.n, X.shape[0]
+        alpha = torch.empty((n, rows), dtype=torch.float64, device=X.device)
+        th, tp = _lib.host_doubles(np.array(self.thetas, dtype=float))
+        jx, jp = _lib.host_doubles(np.array(self.jitters, dtype=float))
+        c = np.arange(n, dtype=np.int32)
+        fv = np.empty(n)
+        ip = ctypes.POINTER(ctypes.c_int32)
+        _lib.check(_lib.lib().nngp_gpfull_lml(
+            X.data_ptr(), rows, n, Y.data_ptr(), n, c.ctypes.data_as(ip), jp, tp, fv.ctypes.data_as(_lib._dp),
+            alpha.data_ptr(), torch.cuda.current_stream().cuda_stream))
+        if np.any(np.isinf(fv)):
+            raise np.linalg.LinAlgError('Matrix is not positive definite')   # np.linalg.cholesky in _predict
+        first = {}
+        for j in range(n):
+            key = tuple(self.thetas[j])
+            if key in first:
+                alpha[j] = alpha[first[key]]
+            else:
+                first[key] = j
+        coef = torch.tensor([[-0.5 * (1 / (sx * sx)), sy * sy] for sx, sy in self.thetas],
+                            dtype=torch.float64, device=X.device)
+        return alpha, coef
+
+    def fit(self, x, y, k, *args, **kwargs):
+        """models.py:420-425."""
+        torch = _lib.require_gpu()
+        self.k = k
+        X = torch.tensor(np.ascontiguousarray(x, dtype=np.float64), device='cuda')
+        Y = torch.tensor(np.ascontiguousarray(y, dtype=np.float64), device='cuda')
+        new_hyp = self._train(X, Y, self.thetas)
+        if k + 1 < self.hyp.shape[-1]:
+            self.hyp[..., k + 1] = new_hyp
+        self.x, self.y = x, y
+        alpha, coef = self._weights(X, Y)
+        self._dev = (X, alpha, coef)
+
+    # ---------------------------------------------------------------------------- prediction
+    def predict_device(self, new_x, out=None, bias=None, stream=None):
+        import torch
+        X, alpha, coef = self._dev
+        if out is None:
+            out = torch.empty(self.n, dtype=torch.float64, device=X.device)
+        st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        _lib.check(_lib.lib().nngp_gpfull_mean(
+            X.data_ptr(), X.shape[0], self.n, new_x.data_ptr(), coef.data_ptr(), alpha.data_ptr(),
+            bias.data_ptr() if bias is not None else None, out.data_ptr(), st))
+        return out
+
+    def predict(self, new_x, prev_F=None, prev_G=None, *args, **kwargs):
+        """models.py:456-462 (host arrays in/out)."""
+        torch = _lib.require_gpu()
+        q = torch.tensor(np.asarray(new_x, dtype=np.float64).reshape(-1), device='cuda')
+        return self.predict_device(q).cpu().numpy()
+
+    def store(self):
+        new = copy.copy(self)
+        new.pool = None
+        new._dev = None
+        new.hyp = self.hyp[..., :self.k + 3]
+        return new
+
+    def state_dict(self):
+        st = super().state_dict()
+        st['settings'] = {'theta': self.theta.tolist(), 'fatol': self.fatol, 'xatol': self.xatol}
+        st.update({'k': self.k, 'thetas': [list(t) for t in self.thetas], 'jitters': self.jitters,
+                   'hyp': self.hyp.tolist(), 'tot_train_t': self.tot_train_t.tolist(),
+                   'train_count': self.train_count.tolist(), 'rng': self.rng.bit_generator.state})
+        return st
+
+    def load_state(self, st):
+        super().load_state(st)
+        self.k = st['k']
+        self.thetas = [tuple(t) for t in st['thetas']]
+        self.jitters = list(st['jitters'])
+        self.hyp = np.array(st['hyp'], dtype=float)
+        self.tot_train_t = np.array(st['tot_train_t'], dtype=float)
+        self.train_count = np.array(st['train_count'], dtype=float)
+        self.rng.bit_generator.state = st['rng']
+
+    def restore_attrs(self, pool):
+        self.pool = pool
+        self._dev = None

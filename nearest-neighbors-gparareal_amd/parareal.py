@@ -25,7 +25,7 @@ import warnings
 import numpy as np
 
 from . import _lib
-from .models import JITTERS, BareParareal, NNGP_p
+from .models import JITTERS, BareParareal, GPjax_p, NNGP_p
 from .solver import SolverAbstr
 from .systems import ODE
 
@@ -156,8 +156,10 @@ class Parareal():
             mdl = BareParareal(N=self.N, **kwargs)
         elif model.lower() == 'nngp':
             mdl = NNGP_p(n=self.n, N=self.N, worker_pool=kwargs['pool'], **kwargs)
-        elif model.lower() in ('gpjax', 'elm'):
-            raise NotImplementedError(f'model {model!r} is outside the nnGP hot path (SURVEY.md §8f)')
+        elif model.lower() == 'gpjax':
+            mdl = GPjax_p(n=self.n, N=self.N, worker_pool=kwargs['pool'], **kwargs)
+        elif model.lower() == 'elm':
+            raise NotImplementedError(f'model {model!r} is outside the GParareal/nnGP path (SURVEY.md §7)')
         else:
             raise Exception('Not implemented')
         s_time = time.time()
@@ -211,6 +213,8 @@ class Parareal():
         mst = state['model']
         if mst['name'] == 'NNGP':
             mdl = NNGP_p(n=self.n, N=self.N, worker_pool=GpuPool(), **mst['settings'])
+        elif mst['name'] == 'GP':
+            mdl = GPjax_p(n=self.n, N=self.N, worker_pool=GpuPool(), **mst['settings'])
         else:
             mdl = BareParareal(N=self.N)
         mdl.load_state(mst)
@@ -258,6 +262,13 @@ class Parareal():
                 ctypes.byref(hits), ctypes.byref(g_ms), stream))
             model.train_count += model.n_fits * (N - I)
             self.spec_hits.append(int(hits.value))
+        elif isinstance(model, GPjax_p):
+            Xg, alpha, coef = model._dev
+            _lib.check(lib.nngp_correction_sweep(
+                ctypes.byref(cs), _lib.TABLEAU[solver.G], solver.step_mode, solver.Ng, t_dev.data_ptr(), I, N,
+                U1.data_ptr(), UG1.data_ptr(), UF.data_ptr(), UG.data_ptr(), _lib.MODEL_GPFULL, Xg.data_ptr(),
+                alpha.data_ptr(), Xg.shape[0], 0, 0, None, 0, coef.data_ptr(), 0.0, 0.0, 0, None, 0, None,
+                ctypes.byref(g_ms), stream))
         else:
             _lib.check(lib.nngp_correction_sweep(
                 ctypes.byref(cs), _lib.TABLEAU[solver.G], solver.step_mode, solver.Ng, t_dev.data_ptr(), I, N,
@@ -278,6 +289,8 @@ class Parareal():
                 j = i - I
                 model.predict_device(X, Y, rows, U1[i], th0[j * nf:(j + 1) * nf], out=U1[i + 1],
                                      bias=UG1[i + 1], stream=stream)
+            elif isinstance(model, GPjax_p):
+                model.predict_device(U1[i], out=U1[i + 1], bias=UG1[i + 1], stream=stream)
             else:   # (uF - uG_prev) + uG_new   (models.py:82-83, parareal.py:382)
                 _lib.check(lib.nngp_parareal_update(self.n, UF[i + 1].data_ptr(), UG[i + 1].data_ptr(),
                                                     UG1[i + 1].data_ptr(), U1[i + 1].data_ptr(), stream))

@@ -12,7 +12,7 @@ this script only chooses inputs and records outputs.  One documented speed subst
 shim's python-loop `vmap` is replaced by a broadcast squared-exponential kernel with the same
 numpy reduction (pairwise sum over the contiguous last axis), so values are unchanged.
 
-Parts: rhs rk lml nm knn preds para_lorenz para_fhn para_burgers rng
+Parts: rhs rk lml nm knn preds para_lorenz para_fhn para_burgers legacy gp rng
 """
 import os
 import sys
@@ -339,6 +339,54 @@ def part_legacy():
     print('legacy nngp 3 iterations', f'{time.time()-st:.1f}s', flush=True)
     _dump_run('lorenz_nngp3', res, arrs)
     save('legacy.npz', **arrs)
+
+
+class GPRecordingPool(RecordingPool):
+    """Records the first `limit` GPjax_p._train fan-outs (models.py:404-407): static inputs
+    (x, y, old thetas, fatol, xatol), the (coordinate, jitter) list and every fit's result."""
+    def map(self, fn, *its, **kw):
+        its = [list(i) if not isinstance(i, itertools.repeat) else i for i in its]
+        res = list(map(fn, *its))
+        if getattr(fn, '__name__', '') == '_get_opt_par' and len(self.calls) < self.limit:
+            static, ins = its
+            st = next(static)
+            self.calls.append(dict(x=np.asarray(st[0]), y=np.asarray(st[1]), old=np.asarray(st[2], dtype=float),
+                                   tol=np.array(st[3:5], dtype=float), ins=np.array(ins, dtype=float),
+                                   res=np.array([r[:-1] for r in res], dtype=float)))
+        return iter(res)
+
+
+def part_gp():
+    """Full-data GParareal (model='gpjax', models.py:273-473) on BASELINE configs[0] (Lorenz N=32),
+    default tolerances (fatol = xatol = 1e-4); records the first two training fan-outs and a few
+    log-likelihood values (GPjax_p.log_lik, models.py:321-327) on the recorded data."""
+    cfg = dict(tspan=[0, 18], N=32, Ng=6, Nf=450, F='RK4', G='RK4', eps=5e-7)
+    arrs = {}
+    ode = rsys.Lorenz(normalization='-11')
+    pool = GPRecordingPool(limit=2)
+    res = _run_para(ode, cfg, 'gpjax', pool=pool)
+    _dump_run('gp', res, arrs)
+    for c, call in enumerate(pool.calls):
+        for k2, v in call.items():
+            arrs[f'call{c}__{k2}'] = v
+    rng = np.random.default_rng(3)
+    c1 = pool.calls[-1]
+    th = np.concatenate([10 ** rng.uniform(-2, 1, (6, 2)), [[1.0, 1.0], [1e-3, 5.0]]])
+    jit = np.array([-20., -16., -12., -13., -20., -11., -15., -20.])
+    lml = np.array([rmodels.GPjax_p.log_lik(c1['x'], c1['y'][:, j % 3], th[j], jit[j]) for j in range(len(th))])
+    arrs['lml_theta'], arrs['lml_jitter'], arrs['lml_val'] = th, jit, lml
+    save('gp_lorenz.npz', **arrs)
+
+
+def part_gp_fhn():
+    """Full-data GParareal on FHN-ODE (configs.py:7-16: N=40, G=RK2 4/slice, F=RK4 4000/slice),
+    a non-chaotic case for exact-K parity."""
+    cfg = dict(tspan=[0, 40], N=40, Ng=4, Nf=4000, F='RK4', G='RK2', eps=5e-7)
+    arrs = {}
+    ode = rsys.FHN_ODE(normalization='-11')
+    res = _run_para(ode, cfg, 'gpjax', pool=GPRecordingPool(limit=0))
+    _dump_run('gp', res, arrs)
+    save('gp_fhn.npz', **arrs)
 
 
 def part_rng():

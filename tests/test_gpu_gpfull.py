@@ -1,0 +1,148 @@
+"""GPU: the full-data GParareal model (models.GPjax_p -> csrc/nngp_gpfull.hip) against the oracle
+(oracle/gpfull.py, pinned to the reference's fixtures) and the reference's own run
+(tests/golden/gp_lorenz.npz: Lorenz N=32, BASELINE configs[0]).
+
+Tolerances: the -LML follows the reference's expressions, but the Cholesky's summation order is
+the GPU's blocked order, not LAPACK's: single values agree to 1e-9 relative; Nelder-Mead
+trajectories that branch on last-bit differences may part, so the fits are compared on the
+selected optimum and the run on K / conv_int / iterates (1e-6)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import gpfull as GF
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(torch, a):
+    return torch.tensor(np.ascontiguousarray(a, dtype=np.float64), device='cuda')
+
+
+def _lml(gpu, torch, x, y, coords, jitters, thetas, alpha=False):
+    n_pts = len(coords)
+    X, Y = _dev(torch, x), _dev(torch, y)
+    c = np.ascontiguousarray(coords, dtype=np.int32)
+    jx = np.ascontiguousarray(jitters, dtype=float)
+    th = np.ascontiguousarray(thetas, dtype=float).reshape(n_pts, 2)
+    fv = np.empty(n_pts)
+    al = torch.empty((n_pts, x.shape[0]), dtype=torch.float64, device='cuda') if alpha else None
+    ip = ctypes.POINTER(ctypes.c_int32)
+    dp = ctypes.POINTER(ctypes.c_double)
+    gpu._lib.check(gpu.lib().nngp_gpfull_lml(
+        X.data_ptr(), x.shape[0], x.shape[1], Y.data_ptr(), n_pts, c.ctypes.data_as(ip), jx.ctypes.data_as(dp),
+        th.ctypes.data_as(dp), fv.ctypes.data_as(dp), al.data_ptr() if alpha else None, None))
+    torch.cuda.synchronize()
+    return fv, (al.cpu().numpy() if alpha else None)
+
+
+def _tol(x, theta, jit):
+    """1e-9 relative, widened by the kernel matrix's condition number (a value at cond ~ 1e20 is
+    roundoff-dominated in any summation order, the reference's included)."""
+    K = GF.gp_kernel(x, x, theta) + np.eye(x.shape[0]) * 10 ** jit
+    with np.errstate(all='ignore'):
+        c = np.linalg.cond(K) if np.all(np.isfinite(K)) else np.inf
+    return max(1e-9, 1e-14 * c) if np.isfinite(c) else 1e-9
+
+
+def _close(a, b, rel):
+    if np.isinf(b):
+        return np.isinf(a) and np.sign(a) == np.sign(b)
+    return abs(a - b) <= rel * max(1.0, abs(b))
+
+
+def test_gpfull_lml_matches_reference_values(gpu):
+    import torch
+    P = golden('gp_lorenz.npz')
+    x, y = P['call1__x'], P['call1__y']
+    k = len(P['lml_val'])
+    fv, _ = _lml(gpu, torch, x, y, [j % 3 for j in range(k)], P['lml_jitter'], P['lml_theta'])
+    for a, b, th, jit in zip(fv, P['lml_val'], P['lml_theta'], P['lml_jitter']):
+        assert _close(a, b, _tol(x, th, jit)), (a, b, th, jit)
+
+
+@pytest.mark.parametrize('n', [1, 5, 31, 32, 33, 64, 100, 257, 600])
+def test_gpfull_lml_and_weights_vs_oracle(gpu, n):
+    """Panel edges (31/32/33), several panels, and a 600-row set (the size GParareal reaches)."""
+    import torch
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-1, 1, (n, 3))
+    y = np.sin(2 * x) + 0.01 * rng.standard_normal((n, 3))
+    thetas = [(0.7, 1.3), (0.2, 0.5), (1.9, 0.05), (0.0, 1.0)]
+    jit = [-12.0, -14.0, -11.0, -16.0]
+    coords = [0, 1, 2, 0]
+    fv, al = _lml(gpu, torch, x, y, coords, jit, thetas, alpha=True)
+    # sigma_x = 0: NaN kernel -> failed Cholesky -> +inf (the reference would raise from
+    # solve_triangular's finite check here, so there is no reference value to compare with)
+    assert np.isinf(fv[3]) and fv[3] > 0
+    for i in range(3):
+        ref = GF.gp_nlml(x, y[:, coords[i]], np.array(thetas[i]), jit[i])
+        assert _close(fv[i], ref, _tol(x, np.array(thetas[i]), jit[i])), (n, i, fv[i], ref)
+        if np.isfinite(ref):   # the weights solve K alpha = y backward-stably (alpha itself is
+            # as ill-conditioned as K, so it is checked through its residual)
+            K = GF.gp_kernel(x, x, np.array(thetas[i])) + np.eye(n) * 10 ** jit[i]
+            yy = y[:, coords[i]]
+            res = np.abs(K @ al[i] - yy).max()
+            assert res <= 1e-12 * (np.abs(K).sum(1).max() * np.abs(al[i]).max() + np.abs(yy).max()), (n, i, res)
+
+
+def test_gpfull_fit_matches_reference_fits(gpu):
+    """nngp_gpfull_fit on the reference's recorded training fan-outs (models.py:404-407): every
+    coordinate's selected optimum (models.py:388-395) matches the reference's."""
+    import torch
+    from nngp_amd.models import JITTERS, _select_fit
+    P = golden('gp_lorenz.npz')
+    m = gpu.GPjax_p(n=3, N=32)
+    for c in (0, 1):
+        x, y, old = P[f'call{c}__x'], P[f'call{c}__y'], P[f'call{c}__old']
+        ins, ref = P[f'call{c}__ins'], P[f'call{c}__res']
+        m.fatol, m.xatol = P[f'call{c}__tol']
+        th, fv, ne = m._fit_batch(_dev(torch, x), _dev(torch, y), [int(i[0]) for i in ins], [i[1] for i in ins],
+                                  [old[int(i[0])] for i in ins])
+        same = np.mean([_close(a, b, 1e-8) for a, b in zip(fv, ref[:, 2])])
+        assert same >= 0.8, f'call{c}: only {same:.0%} of the fits reach the reference fval'
+        for j in range(3):
+            sl = slice(9 * j, 9 * j + 9)
+            g = _select_fit(th[sl], fv[sl], JITTERS)
+            r = _select_fit(ref[sl, :2], ref[sl, 2], JITTERS)
+            assert g[2] == r[2]
+            np.testing.assert_allclose(g[0], r[0], rtol=1e-5, atol=1e-6)
+            assert _close(g[1], r[1], 1e-8)
+
+
+def test_gpfull_predictions_match_oracle(gpu):
+    """After fit() on the reference's second training set, the posterior means (the GPU's
+    weights and gpf_mean_kernel) equal the oracle's for the model's chosen (theta, jitter)."""
+    import torch
+    P = golden('gp_lorenz.npz')
+    x, y = P['call1__x'], P['call1__y']
+    m = gpu.GPjax_p(n=3, N=32)
+    m.thetas = [tuple(t) for t in P['call1__old']]
+    m.fit(x, y, k=1)
+    rng = np.random.default_rng(0)
+    for q in x[:5] + 0.01 * rng.standard_normal((5, 3)):
+        g = m.predict(q)
+        for j in range(3):
+            w = GF.gp_weights(x, y[:, j], np.array(m.thetas[j]), m.jitters[j])
+            o = GF.gp_mean(x, w, q, np.array(m.thetas[j]))
+            assert abs(g[j] - o) <= 1e-7 * max(1.0, abs(o)), (j, g[j], o)
+
+
+def test_gparareal_lorenz_converges_like_reference(gpu):
+    """Parareal(...).run(model='gpjax') on BASELINE configs[0].  Lorenz is chaotic and the
+    reference's own Cholesky order is LAPACK's, so K is compared as a band around the reference's
+    (like the seed spread of nnGP K); the converged solution must equal the serial
+    fine solution (the returned u ends one iterate early, as the reference's does)."""
+    P = golden('gp_lorenz.npz')
+    F = golden('para_lorenz.npz')['fine']
+    ode = gpu.Lorenz(normalization='-11')
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=6, Nf=450, F='RK4', G='RK4')
+    r = gpu.Parareal(ode, s, [0, 18], 32, epsilon=5e-7, verbose=None).run(model='gpjax')
+    print('GParareal K', r['k'], 'reference', int(P['gp__k']), 'conv_int', r['conv_int'],
+          'reference', list(P['gp__conv_int']),
+          'timings', {k: r['timings'][k] for k in ('F_time', 'G_time', 'mdl_tot_t', 'runtime')})
+    assert abs(r['k'] - int(P['gp__k'])) <= 3
+    assert r['conv_int'][-1] == 32
+    np.testing.assert_allclose(r['u'][:, :, -1], F, rtol=0, atol=1e-3)   # u omits the last iterate

@@ -121,3 +121,19 @@ def test_legacy_systems_registry_restates_new_lib():
     assert pts == 450 and iters == [180.0, 180.0, 90.0]
     with pytest.raises(Exception):
         nngp_amd.legacy.LegacySolverRK(f, 7, 100, 1000, 'RK4', 'RK1')   # Ng % N != 0
+
+
+def test_gp_fit_selection_semantics():
+    """GPjax_p's per-coordinate choice (models.py:388-395): fits below 0.9*min (all if none),
+    then Python's min by fval -- first minimum, NaN never chosen unless first, +inf loses."""
+    from nngp_amd.models import _select_fit
+    th = np.arange(18, dtype=float).reshape(9, 2)
+    jit = np.arange(-20, -11, dtype=float)
+    f = np.array([5.0, -3.0, -10.0, -10.0, np.inf, -1.0, 0.0, 2.0, -9.5])
+    assert _select_fit(th, f, jit) == ((4.0, 5.0), -10.0, -18.0)     # first of the tied minima
+    f = np.array([3.0, 2.0, 1.0, 1.0, 4.0, 5.0, 6.0, 7.0, 8.0])        # positive: mask empty -> all
+    assert _select_fit(th, f, jit)[1:] == (1.0, -18.0)
+    f = np.array([np.inf] * 9)
+    assert np.isinf(_select_fit(th, f, jit)[1])
+    f = np.array([np.nan, -5.0, -6.0] + [0.0] * 6)                     # NaN first: kept (min semantics)
+    assert _select_fit(th, f, jit)[2] == -20.0

@@ -267,3 +267,26 @@ def test_fhn_ode_parareal_and_nngp_match_reference():
     # intermediate iterates carry GP roundoff (NM branch flips); the converged column does not
     assert np.nanmax(np.abs(r['u'] - P['nngp_s45__u'])) < 1e-3
     assert np.max(np.abs(r['u'][:, :, -1] - P['nngp_s45__u'][:, :, -1])) < 5e-7   # eps
+
+
+# ---------------------------------------------------------------- full-data GParareal (GPjax_p)
+def test_gp_oracle_fits_match_reference():
+    """oracle/gpfull.py restates GPjax_p's -LML + Nelder-Mead (models.py:306-335); on the
+    reference's own recorded training fan-outs (gen_golden.py part_gp) every fit agrees."""
+    import gpfull as GF
+    P = golden('gp_lorenz.npz')
+    for c in (0, 1):
+        x, y, old, tol = P[f'call{c}__x'], P[f'call{c}__y'], P[f'call{c}__old'], P[f'call{c}__tol']
+        for (j, jit), ref in zip(P[f'call{c}__ins'], P[f'call{c}__res']):
+            th, fv, _ = GF.gp_fit(x, y[:, int(j)], old[int(j)], jit, tol[0], tol[1])
+            np.testing.assert_allclose(th, ref[:2], rtol=1e-12, atol=0)
+            assert fv == pytest.approx(ref[2], rel=1e-12) or (np.isinf(fv) and np.isinf(ref[2]))
+
+
+def test_gp_oracle_lml_matches_reference():
+    import gpfull as GF
+    P = golden('gp_lorenz.npz')
+    x, y = P['call1__x'], P['call1__y']
+    for j, (th, jit, ref) in enumerate(zip(P['lml_theta'], P['lml_jitter'], P['lml_val'])):
+        v = GF.gp_nlml(x, y[:, j % 3], th, jit)
+        assert v == pytest.approx(ref, rel=1e-12) or (np.isinf(v) and np.isinf(ref))
