@@ -146,3 +146,16 @@ def test_gparareal_lorenz_converges_like_reference(gpu):
     assert abs(r['k'] - int(P['gp__k'])) <= 3
     assert r['conv_int'][-1] == 32
     np.testing.assert_allclose(r['u'][:, :, -1], F, rtol=0, atol=1e-3)   # u omits the last iterate
+
+
+def test_gparareal_fhn_ode_matches_reference_K(gpu):
+    """Non-chaotic FHN-ODE (configs.py:7-16: N=40, G=RK2 4/slice, F=RK4 4000/slice): identical
+    K and conv_int as the reference's own GParareal run, iterates to 1e-6."""
+    P = golden('gp_fhn.npz')
+    ode = gpu.FHN_ODE(normalization='-11')
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=4, Nf=4000, F='RK4', G='RK2')
+    r = gpu.Parareal(ode, s, [0, 40], 40, epsilon=5e-7, verbose=None).run(model='gpjax')
+    print('FHN GParareal K', r['k'], 'conv_int', r['conv_int'], 'reference', list(P['gp__conv_int']))
+    assert r['k'] == int(P['gp__k'])
+    assert r['conv_int'] == [int(c) for c in P['gp__conv_int']]
+    np.testing.assert_allclose(r['u'], P['gp__u'], rtol=0, atol=1e-6)
