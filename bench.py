@@ -148,6 +148,23 @@ def converge(torch, g, which):
     return time.perf_counter() - t0, r['k'], r['converged'], r['timings']
 
 
+def gparareal_lorenz(torch, g):
+    """Full-data GParareal (model='gpjax') on BASELINE configs[0], Lorenz N=32.  The reference's
+    own run of this config (tests/golden/gp_lorenz.npz, gen_golden.py part_gp) took 247 s with
+    K = 19 on the 8-core development container; that number is quoted, not re-measured here."""
+    ode = g.Lorenz(normalization='-11')
+    s = g.SolverRK(ode.get_vector_field(), Ng=6, Nf=450, F='RK4', G='RK4')
+    p = g.Parareal(ode, s, [0, 18], 32, epsilon=5e-7, verbose=None)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r = p.run(model='gpjax')
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    return {'wall_s': wall, 'K': r['k'], 'converged': r['converged'], 'mdl_time_s': r['timings']['mdl_tot_t'],
+            'rows': int(r['x'].shape[0]), 'reference_K': 19, 'reference_wall_s_dev_container_8cores': 247.0,
+            'speedup_vs_reference_quoted': 247.0 / wall}
+
+
 def cpu_baseline(steps_per_slice_full, n_slices, target_s=10.0):
     """Oracle C restatement (OpenMP over slices) on a bounded sample of the fine sweep."""
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
@@ -291,6 +308,8 @@ def main():
                                                    'conv_int': tim.get('conv_int', []),
                                                    'spec_hits': tim.get('spec_hits', [])}
             log(which, 'converged', conv, 'K', k, f'{wall:.2f}s')
+        res['gparareal_lorenz_n32'] = gparareal_lorenz(torch, g)
+        log('gparareal lorenz K', res['gparareal_lorenz_n32']['K'], f"{res['gparareal_lorenz_n32']['wall_s']:.2f}s")
         res['burgers_n128_published_schedule'] = burgers_published_schedule(torch, g)
         res['cpu_baseline'] = cpu_baseline(args.steps_per_slice, args.slices_per_gpu)
         # north-star target (>= 10x the CPU path on Burgers N=128, identical K): time the first
