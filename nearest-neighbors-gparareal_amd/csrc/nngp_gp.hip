@@ -716,6 +716,9 @@ struct NMArgs {
     const double *fits_alt2;     //   over fits_alt2 if *skip == 2
     // batched predictions (unfused fits kernel, blockIdx.y = prediction): per-prediction strides
     int64_t qs_D2, qs_Y, qs_th, qs_fits;
+    // unfused fits kernel: per-prediction work queues ([gridDim.y] counters, zeroed) -- a row whose
+    // fit is done takes the next unassigned fit, or NULL (one fit per row)
+    int32_t *queue;
 };
 
 // apply the blockIdx.y prediction offsets of a batched launch (all zero otherwise)
@@ -774,70 +777,86 @@ __global__ void __launch_bounds__(NMBound<MAXM>::T) nm_fit_kernel(NMArgs a) {
         } else {
             f = blockIdx.x * ngroups + g;
             valid = f < a.n_fits;
-            if (valid && a.coord) {
-                coord = a.coord[f];
-                jidx = a.jitter_idx[f];
-            } else if (valid) {   // product(coord, jitter, restart) order (models.py:186)
-                coord = f / nfc;
-                jidx = (f % nfc) / a.R;
-            }
         }
     }
     double y[RPL];
-#pragma unroll
-    for (int s = 0; s < RPL; s++) {
-        const int row = l + 16 * s;
-        y[s] = (valid && row < m) ? a.Y[(int64_t)coord * a.ys_c + (int64_t)row * a.ys_r] : 0.0;
-    }
-    const double jit = valid ? jit_lookup(a, jidx) : 1.0;
+    double jit = 1.0;
     double *Kimg = sK + (size_t)g * IMG;
     GPLane<MAXM> P;
     gp_lane_init<MAXM>(P, m, l);
     gp_image_init<MAXM>(Kimg, m, l);
-
     NMCfg cfg{a.fatol, a.xatol, a.maxfev, a.maxfev};
     NM St;
-    St.fcalls = 0;
-    St.iters = 0;
-    St.f0 = St.f1 = St.f2 = INFINITY;
-    St.xbx = St.xby = St.xrx = St.xry = St.fxr = 0.0;
-    if (valid) {
-        const double t0x = a.theta0[2 * f], t0y = a.theta0[2 * f + 1];
-        St.s0x = t0x; St.s0y = t0y;
-        St.s1x = (t0x != 0) ? (1 + 0.05) * t0x : 0.00025; St.s1y = t0y;   // nonzdelt / zdelt
-        St.s2x = t0x; St.s2y = (t0y != 0) ? (1 + 0.05) * t0y : 0.00025;
-        St.st = ST_INIT0;
-        if (!nm_req(St, cfg, St.s0x, St.s0y, ST_INIT0)) St.st = ST_DONE;
-    } else {
-        St.s0x = St.s0y = St.s1x = St.s1y = St.s2x = St.s2y = 0.0;
-        St.px = St.py = 0.0;
-        St.st = ST_DONE;
-    }
+    // (re)start this row on fit f: its coordinate column, jitter and initial simplex
+    auto start_fit = [&]() {
+        if (!FUSED && valid) {
+            if (a.coord) {
+                coord = a.coord[f];
+                jidx = a.jitter_idx[f];
+            } else {   // product(coord, jitter, restart) order (models.py:186)
+                coord = f / nfc;
+                jidx = (f % nfc) / a.R;
+            }
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < RPL; s2++) {
+            const int row = l + 16 * s2;
+            y[s2] = (valid && row < m) ? a.Y[(int64_t)coord * a.ys_c + (int64_t)row * a.ys_r] : 0.0;
+        }
+        jit = valid ? jit_lookup(a, jidx) : 1.0;
+        St.f0 = St.f1 = St.f2 = INFINITY;
+        St.xbx = St.xby = St.xrx = St.xry = St.fxr = 0.0;
+        if (valid) {
+            nm_start(St, cfg, a.theta0[2 * f], a.theta0[2 * f + 1]);
+        } else {
+            St.s0x = St.s0y = St.s1x = St.s1y = St.s2x = St.s2y = 0.0;
+            St.px = St.py = 0.0;
+            St.fcalls = St.iters = 0;
+            St.st = ST_DONE;
+        }
+    };
+    auto write_fit = [&]() {
+        const double fval = (St.f1 != St.f1 || St.f2 != St.f2) ? NAN : St.f0;
+        if (valid && l == 0) {
+            if (a.theta_out) { a.theta_out[2 * f] = St.s0x; a.theta_out[2 * f + 1] = St.s0y; }
+            if (a.fval_out) a.fval_out[f] = fval;
+            if (a.nfev_out) a.nfev_out[f] = St.fcalls;
+            if (a.fits_out) {
+                a.fits_out[4 * f + 0] = St.s0x;
+                a.fits_out[4 * f + 1] = St.s0y;
+                a.fits_out[4 * f + 2] = fval;
+                a.fits_out[4 * f + 3] = (double)St.fcalls;
+            }
+            if (FUSED) {
+                sRes[4 * g + 0] = St.s0x;
+                sRes[4 * g + 1] = St.s0y;
+                sRes[4 * g + 2] = fval;
+            }
+        }
+    };
+    start_fit();
     // every group of the wave evaluates once per trip until the wave's last fit is done, so the
-    // evaluation code never diverges (finished groups evaluate a dummy point)
+    // evaluation code never diverges (finished groups evaluate a dummy point).  With a work queue
+    // a finished group first takes the next unassigned fit of its prediction (a fit's arithmetic
+    // does not depend on which group runs it), so the wave's groups stay busy to the end.
+    bool can_take = !FUSED && a.queue != nullptr && g < ngroups;
     while (true) {
+        if (!FUSED && can_take && St.st == ST_DONE) {   // uniform within the group
+            write_fit();
+            int fn = 0;
+            if (l == 0) fn = (int)(gridDim.x * ngroups) + atomicAdd(a.queue + blockIdx.y, 1);
+            fn = __builtin_amdgcn_mov_dpp(fn, 0x150, 0xF, 0xF, false);   // row_newbcast:0
+            f = fn;
+            valid = fn < a.n_fits;
+            can_take = valid;
+            start_fit();
+        }
         const bool need = St.st != ST_DONE;
         if (!__any(need)) break;
         const double fv = gp_nlml<MAXM>(m, l, P, sD2, St.px, St.py, jit, y, Kimg);
         if (need) nm_consume(St, cfg, fv);
     }
-    const double fval = (St.f1 != St.f1 || St.f2 != St.f2) ? NAN : St.f0;
-    if (valid && l == 0) {
-        if (a.theta_out) { a.theta_out[2 * f] = St.s0x; a.theta_out[2 * f + 1] = St.s0y; }
-        if (a.fval_out) a.fval_out[f] = fval;
-        if (a.nfev_out) a.nfev_out[f] = St.fcalls;
-        if (a.fits_out) {
-            a.fits_out[4 * f + 0] = St.s0x;
-            a.fits_out[4 * f + 1] = St.s0y;
-            a.fits_out[4 * f + 2] = fval;
-            a.fits_out[4 * f + 3] = (double)St.fcalls;
-        }
-        if (FUSED) {
-            sRes[4 * g + 0] = St.s0x;
-            sRes[4 * g + 1] = St.s0y;
-            sRes[4 * g + 2] = fval;
-        }
-    }
+    write_fit();
     if constexpr (!FUSED) return;
     __syncthreads();
     // first group of each coordinate: first arg-min over its nfc fits (models.py:207-215 reduces
@@ -1123,6 +1142,17 @@ static bool use_spec(int n_fits) {
     return n_fits <= 8 * ncu;
 }
 
+// fits per 16-lane group in the unfused kernel's work-queue mode (NNGP_NM_REFILL; 0/1 = off)
+static int nm_fits_per_row() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("NNGP_NM_REFILL");
+        v = e ? atoi(e) : 8;
+        if (v < 0) v = 0;
+    }
+    return v;
+}
+
 static int run_nm(NMArgs &a, bool fused, hipStream_t st, int nq = 1) {
     const int maxm = maxm_for(a.m);
     const size_t kimg = k_image_doubles(maxm);
@@ -1153,6 +1183,16 @@ static int run_nm(NMArgs &a, bool fused, hipStream_t st, int nq = 1) {
         threads = 256;
         nblocks = (a.n_fits + threads / 16 - 1) / (threads / 16);
         a.cpw = 1;
+        a.queue = nullptr;
+        const int per_row = nm_fits_per_row();
+        if (per_row > 1 && nblocks > 1) {   // work queues: ~per_row fits per group on average
+            int err = 0;
+            int32_t *qbuf = (int32_t *)workspace(sizeof(int32_t) * (size_t)nq, &err, 4);
+            if (err) return err;
+            NNGP_HIP_CHECK(hipMemsetAsync(qbuf, 0, sizeof(int32_t) * (size_t)nq, st));
+            a.queue = qbuf;
+            nblocks = std::max(1, (nblocks + per_row - 1) / per_row);
+        }
     }
     const size_t lds = lds_of(threads);
     switch (maxm) {
