@@ -159,3 +159,16 @@ def test_gparareal_fhn_ode_matches_reference_K(gpu):
     assert r['k'] == int(P['gp__k'])
     assert r['conv_int'] == [int(c) for c in P['gp__conv_int']]
     np.testing.assert_allclose(r['u'], P['gp__u'], rtol=0, atol=1e-6)
+
+
+def test_gparareal_checkpoint_resume_is_bitwise(gpu, tmp_path):
+    """store_int with model='gpjax': resuming from iteration 2's dump restores the warm-start
+    thetas, jitters, hyp and RNG, and reproduces the uninterrupted run exactly."""
+    ode = gpu.Lorenz(normalization='-11')
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=6, Nf=450, F='RK4', G='RK4')
+    full = gpu.Parareal(ode, s, [0, 18], 32, epsilon=5e-7, verbose=None).run(
+        model='gpjax', store_int=True, int_dir=str(tmp_path), int_name='gp', early_stop=6)
+    p = gpu.Parareal(ode, s, [0, 18], 32, epsilon=5e-7, verbose=None)
+    res = p.load_int_dump(str(tmp_path / 'gp_2.npz'), early_stop=6)
+    assert res['k'] == full['k'] and res['conv_int'] == full['conv_int']
+    assert np.array_equal(np.nan_to_num(res['u'], nan=7.0), np.nan_to_num(full['u'], nan=7.0))
