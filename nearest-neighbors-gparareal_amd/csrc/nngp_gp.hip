@@ -760,9 +760,11 @@ __global__ void __launch_bounds__(NMBound<MAXM>::T) nm_fit_kernel(NMArgs a) {
     const int g = tid / 16;                             // group (= DPP row) in block
     const int l = tid % 16;
 
+    __shared__ double sJit[MAX_JIT];   // the jitter powers, so a refill reads one LDS word
     for (int i = tid; i < m * m; i += blockDim.x) sD2[i] = a.D2[i];
     if (FUSED)
         for (int i = tid; i < m; i += blockDim.x) skd2[i] = a.kd2[i];
+    if (tid < MAX_JIT) sJit[tid] = jit_lookup(a, tid);
     __syncthreads();
 
     int f = -1, coord = 0, jidx = 0, q = 0;
@@ -803,7 +805,7 @@ __global__ void __launch_bounds__(NMBound<MAXM>::T) nm_fit_kernel(NMArgs a) {
             const int row = l + 16 * s2;
             y[s2] = (valid && row < m) ? a.Y[(int64_t)coord * a.ys_c + (int64_t)row * a.ys_r] : 0.0;
         }
-        jit = valid ? jit_lookup(a, jidx) : 1.0;
+        jit = valid ? sJit[jidx] : 1.0;
         St.f0 = St.f1 = St.f2 = INFINITY;
         St.xbx = St.xby = St.xrx = St.xry = St.fxr = 0.0;
         if (valid) {
@@ -872,7 +874,7 @@ __global__ void __launch_bounds__(NMBound<MAXM>::T) nm_fit_kernel(NMArgs a) {
             }
         }
         const double sx = sRes[4 * (g + best)], sy = sRes[4 * (g + best) + 1];
-        const double jb = jit_lookup(a, best / a.R);
+        const double jb = sJit[best / a.R];
         const double mean = gp_mean<MAXM>(m, l, P, sD2, skd2, sx, sy, jb, y, Kimg);
         if (l == 0) {
             a.preds[coord] = mean;
