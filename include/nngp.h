@@ -160,6 +160,16 @@ int nngp_predict(const double *X, const double *Y, int64_t rows, int d, const do
                  double *preds_out, const double *bias, double *out, double *fits_out,
                  void *stream);
 
+/* nngp_predict_range: the coordinates [c0, c1) of nngp_predict (their fits, in the same
+ * product order with their own rows of theta0 = the FULL [d*n_jitter*n_restarts][2] draws, and
+ * their means) into preds_out [c1-c0]: a rank's share of one prediction when the multi-GPU
+ * sweep shards the d*9*R fits by coordinate (parareal.correction_sweep_sharded).
+ * Concatenating the ranges gives nngp_predict's preds bit for bit. */
+int nngp_predict_range(const double *X, const double *Y, int64_t rows, int d, const double *new_x,
+                       int m, int n_jitter, const double *jitter_exp_host, int n_restarts,
+                       const double *theta0, int c0, int c1, double fatol, double xatol, int maxfev,
+                       double *preds_out, void *stream);
+
 /* ---- 3. the sequential correction sweep of one Parareal iteration ------------------------
  * Replaces the loop parareal.py:359-382 (legacy new_lib.py:990-1012): for i = I .. N-1
  *     UG1[i+1] = G(t[i], t[i+1], U1[i])                     run_G_timed, parareal.py:361

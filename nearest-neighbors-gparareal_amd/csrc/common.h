@@ -56,7 +56,7 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
                  double fatol, double xatol, int maxfev, double *preds_out, const double *bias,
                  double *out, double *fits_out, const int32_t *spec_idx, const double *spec_fits,
                  int32_t *hit_flag, const int32_t *spec2_idx, const double *spec2_fits, int32_t *host_flag,
-                 hipStream_t st);
+                 hipStream_t st, int c0 = 0, int c1 = -1);
 int gpfull_mean(const double *X, int64_t rows, int d, const double *q, const double *coef, const double *alpha,
                 const double *bias, double *out, hipStream_t st);
 int spec_batch(const double *X, const double *Y, int64_t rows, int d, const double *Q, int nq, int m,

@@ -1293,8 +1293,10 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
                  double fatol, double xatol, int maxfev, double *preds_out, const double *bias,
                  double *out, double *fits_out, const int32_t *spec_idx, const double *spec_fits,
                  int32_t *hit_flag, const int32_t *spec2_idx, const double *spec2_fits, int32_t *host_flag,
-                 hipStream_t st) {
+                 hipStream_t st, int c0, int c1) {
     NNGP_REQUIRE(X && Y && new_x && theta0 && preds_out, "null array argument");
+    if (c1 < 0) c1 = d;
+    NNGP_REQUIRE(0 <= c0 && c0 < c1 && c1 <= d, "bad coordinate range [%d, %d) of d=%d", c0, c1, d);
     NNGP_REQUIRE(m >= 1 && m <= 32, "need 1 <= m <= 32 (got %d)", m);
     NNGP_REQUIRE(m <= rows, "m=%d exceeds training rows=%lld", m, (long long)rows);
     NNGP_REQUIRE(d >= 1 && n_restarts >= 1 && maxfev >= 1, "bad d / n_restarts / maxfev");
@@ -1323,9 +1325,14 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
                       spec ? hit_flag : (int32_t *)nullptr, knn_xs_doubles(m, d),
                       spec ? spec2_idx : (const int32_t *)nullptr, spec ? host_flag : (int32_t *)nullptr);
     NNGP_LAUNCH_CHECK();
-    a.m = m; a.d = d; a.n_fits = (int)n_fits;
-    a.D2 = D2; a.kd2 = kd2; a.Y = ymT; a.ys_c = m; a.ys_r = 1;
-    a.theta0 = theta0; a.fatol = fatol; a.xatol = xatol; a.maxfev = maxfev; a.R = n_restarts;
+    // coordinates [c0, c1) only (the multi-rank sweep's share): the fits and means of those
+    // columns, in the same product(coord, jitter, restart) order with their own theta0 draws
+    const int dc = c1 - c0;
+    const size_t nfc = (size_t)n_jitter * n_restarts;
+    a.m = m; a.d = dc; a.n_fits = (int)(dc * nfc);
+    a.D2 = D2; a.kd2 = kd2; a.Y = ymT + (size_t)c0 * m; a.ys_c = m; a.ys_r = 1;
+    a.theta0 = theta0 + (size_t)c0 * nfc * 2; a.fatol = fatol; a.xatol = xatol; a.maxfev = maxfev;
+    a.R = n_restarts;
     a.fits_out = fits_out ? fits_out : fits_ws;
     a.preds = preds_out; a.bias = bias; a.out = out;
     if (spec) {
@@ -1400,5 +1407,14 @@ extern "C" int nngp_predict(const double *X, const double *Y, int64_t rows, int 
                             void *stream) {
     return nngp::predict_impl(X, Y, rows, d, new_x, m, n_jitter, jitter_exp_host, n_restarts, theta0, fatol,
                               xatol, maxfev, preds_out, bias, out, fits_out, nullptr, nullptr, nullptr, nullptr,
-                              nullptr, nullptr, (hipStream_t)stream);
+                              nullptr, nullptr, (hipStream_t)stream, 0, d);
+}
+
+extern "C" int nngp_predict_range(const double *X, const double *Y, int64_t rows, int d, const double *new_x,
+                                  int m, int n_jitter, const double *jitter_exp_host, int n_restarts,
+                                  const double *theta0, int c0, int c1, double fatol, double xatol, int maxfev,
+                                  double *preds_out, void *stream) {
+    return nngp::predict_impl(X, Y, rows, d, new_x, m, n_jitter, jitter_exp_host, n_restarts, theta0, fatol,
+                              xatol, maxfev, preds_out, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                              nullptr, nullptr, nullptr, (hipStream_t)stream, c0, c1);
 }

@@ -110,6 +110,41 @@ def fine_sweep_sharded(propagate, t, U, UF, I, N, group=None):
     UF[I + 1:N + 1] = gathered[:N - I]
 
 
+def _all_gather_flat(send, group, world):
+    """All-gather of equal-size 1-D/2-D blocks in rank order (RCCL all_gather_into_tensor, or
+    the list form on gloo)."""
+    import torch
+    dist = torch.distributed
+    if dist.get_backend(group) == 'gloo':
+        parts = [torch.empty_like(send) for _ in range(world)]
+        dist.all_gather(parts, send, group=group)
+        return torch.cat(parts)
+    out = torch.empty((world * send.shape[0],) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
+    dist.all_gather_into_tensor(out, send, group=group)
+    return out
+
+
+def correction_sweep_sharded(coarse, predict_range, assemble, I, N, U1, UG1, d, group=None):
+    """The sequential correction sweep (parareal.py:359-382) with each prediction's d*9*R fits
+    sharded by coordinate over the ranks of `group` (worth it when d*9 is large,
+    FHN-PDE d=800 has 7200 fits per prediction).  Per slice i: every rank runs the coarse step
+    `coarse(i, U1[i], UG1[i+1])` (replicated, deterministic), its own coordinate block
+    `predict_range(i, c0, c1, U1[i], out)`, ONE all-gather of the [chunk] predictions, and
+    `assemble(preds[:d], UG1[i+1], U1[i+1])` (u = preds + uG).  Ranks stay bit-identical."""
+    import torch
+    dist = torch.distributed
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    c0, c1, chunk = shard_bounds(0, d, world, rank)
+    send = torch.zeros(chunk, dtype=U1.dtype, device=U1.device)
+    for i in range(I, N):
+        coarse(i, U1[i], UG1[i + 1])
+        if c1 > c0:
+            predict_range(i, c0, c1, U1[i], send[:c1 - c0])
+        preds = _all_gather_flat(send, group, world)
+        assemble(preds[:d], UG1[i + 1], U1[i + 1])
+
+
 class Parareal():
 
     def __init__(self, ode, solver, tspan, N, epsilon=5e-7, verbose='v', process_group=None, **kwargs):
@@ -132,6 +167,7 @@ class Parareal():
         self.process_group = process_group
         # nnGP sweep speculation (include/nngp.h nngp_correction_sweep): -1 auto, 0 off, 1 on
         self.speculate = int(kwargs.get('speculate', -1))
+        self.shard_corrections = kwargs.get('shard_corrections')
         self.spec_hits = []
 
     def _get_pool(self, *args, **kwargs):
@@ -248,6 +284,8 @@ class Parareal():
                                              th0, stream)
         cs = solver.f.csystem(U1.device)
         g_ms = ctypes.c_float(0.0)
+        if isinstance(model, NNGP_p) and self._shard_corrections(model):
+            return self._correction_sweep_sharded(torch, model, t_dev, I, N, U1, UG1, X, Y, rows, th0, stream)
         if isinstance(model, NNGP_p):
             m = min(model.n_neighbours(), int(rows))
             jit, jp = _lib.host_doubles(JITTERS)
@@ -275,6 +313,51 @@ class Parareal():
                 U1.data_ptr(), UG1.data_ptr(), UF.data_ptr(), UG.data_ptr(), _lib.MODEL_PARAREAL, None, None,
                 0, 0, 0, None, 0, None, 0.0, 0.0, 0, None, 0, None, ctypes.byref(g_ms), stream))
         return g_ms.value / 1e3
+
+    def _shard_corrections(self, model):
+        """Shard each prediction's fits by coordinate over the process group: run(...,
+        shard_corrections=True/False), default when more than one rank and d*9*R >= 2048."""
+        import torch
+        dist = torch.distributed
+        if self.process_group is None and not (dist.is_available() and dist.is_initialized()):
+            return False
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(self.process_group) == 1:
+            return False
+        if self.shard_corrections is not None:
+            return bool(self.shard_corrections)
+        return model.n_fits >= 2048
+
+    def _correction_sweep_sharded(self, torch, model, t_dev, I, N, U1, UG1, X, Y, rows, th0, stream):
+        """correction_sweep_sharded with the HIP launches: G via the solver, nngp_predict_range
+        for this rank's coordinates, u = (preds - 0) + uG via nngp_parareal_update (bitwise the
+        fused kernel's mean + uG)."""
+        lib, solver, n = _lib.lib(), self.solver, self.n
+        m = min(model.n_neighbours(), int(rows))
+        jit, jp = _lib.host_doubles(JITTERS)
+        nf = model.n_fits
+        zeros = torch.zeros(n, dtype=torch.float64, device=U1.device)
+        ev = _Events(torch)
+
+        def coarse(i, u, out):
+            eg = ev.start()
+            solver.run_G_batch(t_dev[i:i + 1], t_dev[i + 1:i + 2], u.view(1, -1), out=out.view(1, -1))
+            ev.stop(eg, 'G')
+
+        def predict_range(i, c0, c1, u, out):
+            j = i - I
+            _lib.check(lib.nngp_predict_range(
+                X.data_ptr(), Y.data_ptr(), int(rows), n, u.data_ptr(), m, len(jit), jp, model.n_restarts,
+                th0[j * nf:(j + 1) * nf].data_ptr(), c0, c1, float(model.fatol), float(model.xatol), model.maxfev,
+                out.data_ptr(), stream))
+
+        def assemble(preds, ug, out):
+            _lib.check(lib.nngp_parareal_update(n, preds.data_ptr(), zeros.data_ptr(), ug.data_ptr(),
+                                                out.data_ptr(), stream))
+
+        correction_sweep_sharded(coarse, predict_range, assemble, I, N, U1, UG1, n, self.process_group)
+        model.train_count += nf * (N - I)
+        self.spec_hits.append(0)
+        return ev.collect().get('G', 0.0)
 
     def _correction_sweep_py(self, torch, model, t_dev, I, N, U1, UG1, UF, UG, X, Y, rows, th0, stream):
         """Per-slice Python loop (paged coarse solver only): same launches, issued one by one."""

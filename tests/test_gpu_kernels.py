@@ -246,3 +246,35 @@ def test_predict_every_padded_size_and_fallback_vs_oracle(gpu, m, d, R):
     assert np.array_equal(fits.cpu().numpy(), ofits)
     assert np.array_equal(preds, ora)
     assert np.array_equal(out.cpu().numpy(), ora + bias)
+
+
+@pytest.mark.parametrize('d,R,world', [(3, 1, 2), (128, 1, 3), (300, 1, 8), (130, 2, 4)])
+def test_predict_range_blocks_concatenate_to_predict(gpu, d, R, world):
+    """nngp_predict_range over the coordinate blocks of shard_bounds (the multi-rank sweep's
+    shares) concatenates to nngp_predict bit for bit -- the spec, packed and split fit paths."""
+    import ctypes
+    import torch
+    from nngp_amd.models import JITTERS
+    from nngp_amd.parareal import shard_bounds
+    m = 15
+    rng = np.random.default_rng(d + R)
+    X = np.cumsum(0.05 * rng.standard_normal((4 * m, d)), axis=0)
+    Y = 0.01 * np.sin(3 * X) + 1e-5 * rng.standard_normal(X.shape)
+    q = X[m] + 0.01
+    mdl = gpu.NNGP_p(n=d, N=4, nn=m, n_restarts=R, seed=3)
+    th0 = _t(torch, mdl.draw_thetas(1))
+    Xt, Yt, qt = _t(torch, X), _t(torch, Y), _t(torch, q)
+    full = mdl.predict_device(Xt, Yt, X.shape[0], qt, th0).cpu().numpy()
+    jit = np.ascontiguousarray(JITTERS)
+    parts = []
+    for r in range(world):
+        c0, c1, _ = shard_bounds(0, d, world, r)
+        if c1 <= c0:
+            continue
+        out = torch.empty(c1 - c0, dtype=torch.float64, device='cuda')
+        gpu._lib.check(gpu.lib().nngp_predict_range(
+            Xt.data_ptr(), Yt.data_ptr(), X.shape[0], d, qt.data_ptr(), m, len(jit),
+            jit.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), R, th0.data_ptr(), c0, c1, 0.1, 0.1, 400,
+            out.data_ptr(), None))
+        parts.append(out.cpu().numpy())
+    assert np.array_equal(np.concatenate(parts), full)
