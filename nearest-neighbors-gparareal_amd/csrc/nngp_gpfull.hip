@@ -28,8 +28,11 @@
 #include "nngp_nm.h"
 
 namespace nngp {
+#ifndef GPF_PANEL
+#define GPF_PANEL 32
+#endif
 
-static constexpr int GPB = 32;                       // panel width
+static constexpr int GPB = GPF_PANEL;                // panel width
 static constexpr double GPF_LOG_2PI = 1.8378770664093453;   // np.log(2*np.pi)
 static constexpr int GPF_MAX_ROWS = 7936;            // alpha_kernel keeps the vector in LDS (<= 62 KB)
 
