@@ -278,3 +278,21 @@ def test_predict_range_blocks_concatenate_to_predict(gpu, d, R, world):
             out.data_ptr(), None))
         parts.append(out.cpu().numpy())
     assert np.array_equal(np.concatenate(parts), full)
+
+
+@pytest.mark.parametrize('nx,n_slices,norm', [(20, 512, False), (20, 64, True), (22, 8, False)])
+def test_fhn_pde_full_size_vs_oracle(gpu, nx, n_slices, norm):
+    """BASELINE configs[4]'s FHN-PDE at its full size (d = 2*20^2 = 800, 512 slices; the 8-GPU
+    share of 64 slices; and d = 968 near the 512-thread form's limit), RK8: sampled slices are
+    bitwise the oracle's."""
+    import torch
+    ode = gpu.FHN_PDE(d_x=nx, normalization='-11' if norm else None)
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=1, Nf=6, F='RK8', G='RK1')
+    rng = np.random.default_rng(nx + n_slices)
+    U0 = np.clip(ode.get_init_cond()[None, :] + 0.01 * rng.standard_normal((n_slices, ode.d)), -1, 1)
+    T = np.arange(n_slices + 1) * 6e-3      # 1e-3 per RK8 step: inside the explicit stability region
+    out = s.run_F_batch(_t(torch, T[:-1]), _t(torch, T[1:]), _t(torch, U0)).cpu().numpy()
+    so = O.System('fhn_pde', nx=nx, mn=-1, mx=1) if norm else O.System('fhn_pde', nx=nx, normalized=False)
+    assert np.all(np.isfinite(out))
+    for i in sorted({0, 1, n_slices // 2, n_slices - 1}):
+        assert np.array_equal(out[i], so.rk(8, T[i], T[i + 1], 6, U0[i], O.STEP_FIXED)), i
