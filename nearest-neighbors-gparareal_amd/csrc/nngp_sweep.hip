@@ -257,7 +257,8 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
             respec_pending = true;
         }
     }
-    if (respec_pending && rc == NNGP_OK) NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_r, 0));
+    // the side stream never outlives the sweep (also on an error path: its buffers are reused)
+    if (respec_pending) NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_r, 0));
     if (spec_hits_out && rc == NNGP_OK) {   // speculation hits (0 when not speculating)
         *spec_hits_out = 0;
         if (spec) {
