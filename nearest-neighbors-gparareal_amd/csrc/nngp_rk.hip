@@ -562,7 +562,7 @@ static int launch_field_ept(const FieldArgs &fa, int bt, int n, const double *t0
 
 // threads per slice: env NNGP_RK_THREADS overrides (tuning), else the fewest whole waves that
 // keep EPT <= 4 (d=128 -> 64 threads x 2, d=800 -> 256 threads x 4)
-static int pick_threads(int d) {
+static int pick_threads(int d, int n_slices) {
     const char *env = getenv("NNGP_RK_THREADS");
     if (env) {
         int v = atoi(env);
@@ -570,9 +570,13 @@ static int pick_threads(int d) {
     }
     int bt = 64;
     while (bt < 256 && (d + bt - 1) / bt > 4) bt += 64;
-    // up to 1024 elements: <= 2 per thread in a 512-thread workgroup -- twice the waves per
-    // slice to hide the stage chain's latency (FHN-PDE d=800, 512 slices: 8.6 -> 6.6 us/step)
-    if ((d + bt - 1) / bt > 2 && d <= 1024) bt = 512;
+    // up to 1024 elements: one element per thread while all slices' waves fit ~4 per SIMD (few
+    // slices: the per-step latency is the stage chain, FHN-PDE d=800 at 64 slices 5.2 -> 4.0
+    // us/step), else <= 2 per thread in 512 threads (512 slices: 8.6 -> 6.7 us/step)
+    if ((d + bt - 1) / bt > 2 && d <= 1024) {
+        const int64_t waves1 = (int64_t)n_slices * ((d + 63) / 64);
+        bt = (waves1 <= 4 * 1024) ? ((d + 63) / 64) * 64 : 512;
+    }
     return bt;
 }
 
@@ -631,7 +635,7 @@ static int launch_field(const nngp_system *sys, int n, const double *t0, const d
         if (e == 3) return launch_burgers_wave<ORDER, LIN, 3>(fa, n, t0, t1, steps, gsteps, j0, u0, uF, st);
         return launch_burgers_wave<ORDER, LIN, 4>(fa, n, t0, t1, steps, gsteps, j0, u0, uF, st);
     }
-    const int bt = pick_threads(sys->d);
+    const int bt = pick_threads(sys->d, n);
     const int ept = (sys->d + bt - 1) / bt;
     NNGP_REQUIRE(ept <= 8, "d=%d too large for the field kernel (max 2048)", sys->d);
     if (ept <= 1) return launch_field_ept<SYS, ORDER, LIN, 1>(fa, bt, n, t0, t1, steps, gsteps, j0, u0, uF, st);

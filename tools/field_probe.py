@@ -40,3 +40,4 @@ if __name__ == '__main__':
     torch.cuda.set_device(0)
     sweep('burgers', g.Burgers(d_x=128, normalization='-11'), 128, 2000, [0, 5])
     sweep('fhn', g.FHN_PDE(d_x=20), 512, 2000, [0, 1100])
+    sweep('fhn', g.FHN_PDE(d_x=20), 64, 2000, [0, 1100 / 8])   # one GPU's share of N=512 on 8 GPUs
