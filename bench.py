@@ -148,6 +148,32 @@ def converge(torch, g, which):
     return time.perf_counter() - t0, r['k'], r['converged'], r['timings']
 
 
+def corrections_fhn_d200(torch, g, n_pred=20):
+    """nnGP corrections at the FHN-PDE d=200 shape (m=20, R=1: 1 800 fits per prediction) on a
+    synthetic 3 000-row training set, one prediction after another on one GPU.  BASELINE.md §B
+    derives 1.54 corrections/s for the reference's FHN d=200 N=512 run on 517 cores."""
+    d, rows, m = 200, 3000, 20
+    rng = np.random.default_rng(0)
+    X = np.cumsum(0.02 * rng.standard_normal((rows, d)), axis=0)
+    Y = 0.01 * np.sin(3 * X)
+    dev = lambda a: torch.tensor(a, dtype=torch.float64, device='cuda')
+    Xt, Yt = dev(X), dev(Y)
+    mdl = g.NNGP_p(n=d, N=n_pred, nn=m, n_restarts=1, seed=45)
+    th0 = dev(mdl.draw_thetas(n_pred + 1))
+    nf = mdl.n_fits
+    out = torch.empty(d, dtype=torch.float64, device='cuda')
+    mdl.predict_device(Xt, Yt, rows, Xt[0] + 1e-3, th0[:nf], out=out, bias=out)   # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(n_pred):
+        mdl.predict_device(Xt, Yt, rows, Xt[(37 * j) % rows] + 1e-3, th0[(j + 1) * nf:(j + 2) * nf])
+    torch.cuda.synchronize()
+    s = time.perf_counter() - t0
+    return {'corrections_per_s': n_pred / s, 'ms_per_correction': s / n_pred * 1e3, 'd': d, 'm': m,
+            'rows': rows, 'fits_per_correction': nf, 'reference_corrections_per_s_517_cores': 1.54,
+            'ratio_vs_reference': n_pred / s / 1.54}
+
+
 def gparareal_lorenz(torch, g):
     """Full-data GParareal (model='gpjax') on BASELINE configs[0], Lorenz N=32.  The reference's
     own run of this config (tests/golden/gp_lorenz.npz, gen_golden.py part_gp) took 247 s with
@@ -308,6 +334,9 @@ def main():
                                                    'conv_int': tim.get('conv_int', []),
                                                    'spec_hits': tim.get('spec_hits', [])}
             log(which, 'converged', conv, 'K', k, f'{wall:.2f}s')
+        res['nngp_corrections_fhn_d200'] = corrections_fhn_d200(torch, g)
+        res['nngp_corrections_hopf_vs_reference'] = {'reference_corrections_per_s_141_cores': 44.0,
+                                                      'ratio': res['nngp_corrections_per_s'] / 44.0}
         res['gparareal_lorenz_n32'] = gparareal_lorenz(torch, g)
         log('gparareal lorenz K', res['gparareal_lorenz_n32']['K'], f"{res['gparareal_lorenz_n32']['wall_s']:.2f}s")
         res['burgers_n128_published_schedule'] = burgers_published_schedule(torch, g)
