@@ -20,7 +20,6 @@ import ctypes
 import json
 import os
 import time
-import warnings
 
 import numpy as np
 
@@ -359,6 +358,39 @@ class Parareal():
         self.spec_hits.append(0)
         return ev.collect().get('G', 0.0)
 
+    def _correction_sweep_debug(self, torch, model, t_dev, I, N, U1, UG1, UF, UG, X, Y, rows, th0, stream):
+        """debug=True (parareal.py:353-392): the same per-slice sweep, keeping every prediction,
+        then the 'truth' F(u[i]) - uG_new[i+1] for all slices at once -- ONE batched fine launch
+        instead of the reference's N-I serial run_F calls -- and |truth - preds| per slice and
+        coordinate.  Returns (G seconds, pred_err [N-I][n])."""
+        lib, n = _lib.lib(), self.n
+        P = torch.empty((N - I, n), dtype=torch.float64, device=U1.device)
+        zeros = torch.zeros(n, dtype=torch.float64, device=U1.device)
+        ev = _Events(torch)
+        nf = model.n_fits if isinstance(model, NNGP_p) else 0
+        for i in range(I, N):
+            j = i - I
+            eg = ev.start()
+            self.solver.run_G_batch(t_dev[i:i + 1], t_dev[i + 1:i + 2], U1[i:i + 1], out=UG1[i + 1:i + 2])
+            ev.stop(eg, 'G')
+            if isinstance(model, NNGP_p):
+                model.predict_device(X, Y, rows, U1[i], th0[j * nf:(j + 1) * nf], out=U1[i + 1],
+                                     bias=UG1[i + 1], preds=P[j], stream=stream)
+            else:
+                if isinstance(model, GPjax_p):
+                    model.predict_device(U1[i], out=P[j], stream=stream)
+                else:   # BareParareal: uF - uG (models.py:82-83)
+                    _lib.check(lib.nngp_parareal_update(n, UF[i + 1].data_ptr(), UG[i + 1].data_ptr(), None,
+                                                        P[j].data_ptr(), stream))
+                _lib.check(lib.nngp_parareal_update(n, P[j].data_ptr(), zeros.data_ptr(), UG1[i + 1].data_ptr(),
+                                                    U1[i + 1].data_ptr(), stream))
+        truth = torch.empty((N - I, n), dtype=torch.float64, device=U1.device)
+        self.solver.run_F_batch(t_dev[I:N], t_dev[I + 1:N + 1], U1[I:N].contiguous(), out=truth)
+        _lib.check(lib.nngp_parareal_update((N - I) * n, truth.data_ptr(), UG1[I + 1:N + 1].data_ptr(), None,
+                                            truth.data_ptr(), stream))
+        pred_err = np.abs(truth.cpu().numpy() - P.cpu().numpy())
+        return ev.collect().get('G', 0.0), pred_err
+
     def _correction_sweep_py(self, torch, model, t_dev, I, N, U1, UG1, UF, UG, X, Y, rows, th0, stream):
         """Per-slice Python loop (paged coarse solver only): same launches, issued one by one."""
         lib = _lib.lib()
@@ -383,8 +415,9 @@ class Parareal():
     def _parareal(self, model, debug=False, early_stop=None, parall='Serial', store_int=False,
                   _resume=None, **kwargs):
         torch = _lib.require_gpu()
-        if debug:
-            warnings.warn('debug mode (per-slice fine re-solves) is not supported; ignored')
+        if debug and self.process_group is not None:
+            raise NotImplementedError('debug mode runs on one rank')
+        one_step_error, all_pred_err = [], []   # debug (parareal.py:258-262)
         self.spec_hits = []
         tspan, N, epsilon, n = self.tspan, self.N, self.epsilon, self.n
         solver = self.solver
@@ -495,8 +528,15 @@ class Parareal():
             if is_nngp:
                 th0 = torch.tensor(model.draw_thetas(N - I), **f64)
             e_loop = ev.start()
-            g_s = self._correction_sweep(torch, model, t_dev, I, N, Uk1, UGk1, UF, UGk, Xs, Ds, rows_s,
-                                         th0 if is_nngp else None, stream)
+            if debug:
+                g_s, pred_err = self._correction_sweep_debug(torch, model, t_dev, I, N, Uk1, UGk1, UF, UGk, Xs, Ds,
+                                                             rows_s, th0 if is_nngp else None, stream)
+                if verbose == 'v':
+                    print(f'Avg error {np.mean(pred_err, 0)}, Max. error {np.max(pred_err, 0)}')
+                all_pred_err.append(pred_err)
+            else:
+                g_s = self._correction_sweep(torch, model, t_dev, I, N, Uk1, UGk1, UF, UGk, Xs, Ds, rows_s,
+                                             th0 if is_nngp else None, stream)
             ev.stop(e_loop, 'loop')
             u[:, :, k + 1] = Uk1.cpu().numpy()
             ug = UGk1.cpu().numpy()
@@ -507,6 +547,8 @@ class Parareal():
                 raise Exception('NaN values in initial coarse solve - increase Ng!')
             err[:, k] = np.linalg.norm(u[:, :, k + 1] - u[:, :, k], np.inf, 1)   # (:402-403)
             err[I, k] = 0
+            if debug:   # (:405-406)
+                one_step_error.append([err[I + 1, k], pred_err.max()])
             II = I
             for p in range(II + 1, N + 1):                                          # (:408-416)
                 if err[p, k] < epsilon:
@@ -535,6 +577,9 @@ class Parareal():
         timings = {'F_time': F_time, 'G_time': G_time, 'F_time_serial_avg': F_time_serial,
                    'spec_hits': list(self.spec_hits)}
         timings.update(model.get_times())
+        debug_dict = {}
+        if debug:   # (:441-463; the reference also plots these)
+            debug_dict = {'one_step_error': np.array(one_step_error), 'all_pred_err': all_pred_err}
         return {'t': t, 'u': u[:, :, :k + 1], 'err': err[:, :k + 1], 'x': x, 'D': D, 'k': k + 1,
                 'data_x': data_x[..., :k + 1], 'data_D': data_D[..., :k + 1], 'timings': timings,
-                'debug_dict': {}, 'converged': I == N, 'conv_int': conv_int}
+                'debug_dict': debug_dict, 'converged': I == N, 'conv_int': conv_int}

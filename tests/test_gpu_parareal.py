@@ -143,3 +143,25 @@ def test_speculative_sweep_is_bitwise_and_hits(gpu, case, window, monkeypatch):
     hits = b['timings']['spec_hits']
     print(case, window, 'speculation hits per iteration', hits)
     assert sum(hits) > 0 and a['timings']['spec_hits'] == [0] * len(hits)
+
+
+@pytest.mark.parametrize('model', ['nngp', 'parareal', 'gpjax'])
+def test_debug_mode_reports_prediction_errors_without_changing_the_run(gpu, model):
+    """run(debug=True) (parareal.py:258-262, 353-406, 441-463): the same iterates, plus per
+    iteration |F(u_i) - uG_new - prediction| for every slice and the one-step error table."""
+    ode = gpu.Lorenz(normalization='-11')
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=6, Nf=450, F='RK4', G='RK4')
+    kw = dict(nn=10, seed=46) if model == 'nngp' else {}
+    a = gpu.Parareal(ode, s, [0, 18], 32, epsilon=5e-7, verbose=None).run(model=model, early_stop=4, **kw)
+    b = gpu.Parareal(ode, s, [0, 18], 32, epsilon=5e-7, verbose=None).run(model=model, early_stop=4, debug=True,
+                                                                          **kw)
+    assert a['debug_dict'] == {}
+    assert np.array_equal(np.nan_to_num(a['u'], nan=7.0), np.nan_to_num(b['u'], nan=7.0))
+    dd = b['debug_dict']
+    assert dd['one_step_error'].shape == (b['k'], 2)
+    assert len(dd['all_pred_err']) == b['k']
+    I = 1
+    for k, pe in enumerate(dd['all_pred_err']):
+        assert pe.shape == (32 - I, 3) and np.all(np.isfinite(pe))
+        I = b['conv_int'][k] + 1   # the next sweep starts after the next F increment
+    assert np.all(dd['one_step_error'][:, 1] == [pe.max() for pe in dd['all_pred_err']])
