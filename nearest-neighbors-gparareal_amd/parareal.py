@@ -264,6 +264,77 @@ class Parareal():
         self.runs[cstm_mdl_name or mdl.name] = out
         return out
 
+    # ------------------------------------------------------------------------------ reports
+    def _fine_reference(self):
+        """The serial fine solve the reports compare against (parareal.py:636-643): run_F_timed
+        over the whole span from u0, cached in self.fine / self.fine_t."""
+        if self.fine is None:
+            self.fine, self.fine_t = self.solver.run_F_timed(self.tspan[0], self.tspan[-1], self.u0)
+        return self.fine_t
+
+    def print_times(self, mdl_speedup=None, expected_fine=None):
+        """Markdown table of K, G/F/model times, runtime and speed-up of every run in self.runs
+        (parareal.py:636-694): speed-up against the serial fine solve, or -- with mdl_speedup =
+        a run name -- model-time speed-up against that run; expected_fine adds the speed-up
+        expected from the fine cost alone."""
+        ref_mdl = self.runs[mdl_speedup]['timings']['mdl_tot_t'] if mdl_speedup in self.runs else None
+        fine_t = None if ref_mdl is not None else self._fine_reference()
+        keys = ['G_time', 'F_time', 'mdl_train_t', 'mdl_pred_t', 'mdl_tot_t', 'runtime']
+        head = ['Model', 'K', 'G', 'F', 'Train', 'Pred', 'Mdl Tot', 'Overall',
+                'Mdl Speedup' if ref_mdl is not None else 'Speedup']
+        if expected_fine is not None:
+            head.append('E[Speedup]')
+        rows = [['Fine'] + ['-'] * 6 + (['-', '-'] if ref_mdl is not None else [f'{fine_t:.2e}', '1'])]
+        if expected_fine is not None:
+            rows[0].append('1')
+        for name, v in self.runs.items():
+            tm = v['timings']
+            row = [name, str(v['k'])] + [f'{tm[k]:.2e}' for k in keys]
+            row.append(f'{(ref_mdl / tm["mdl_tot_t"]) if ref_mdl is not None else (fine_t / tm["runtime"]):.2f}')
+            if expected_fine is not None:
+                row.append(f'{expected_fine / (expected_fine / self.N * v["k"] + tm["mdl_tot_t"]):.2f}')
+            rows.append(row)
+        width = [max(len(r[i]) for r in [head] + rows) for i in range(len(head))]
+        line = lambda r: '|' + '|'.join(f'{x:^{w}}' for x, w in zip(r, width)) + '|'
+        out = '\n'.join([line(head), '|' + '|'.join('-' * w for w in width) + '|'] + [line(r) for r in rows])
+        print(out)
+        return out
+
+    def print_speedup(self, mdls=None, md=True, fine_t=None, F_t=None, mdl_title=''):
+        """Speed-up table (parareal.py:697-758), markdown (md=True) or a LaTeX tabular: per run
+        K, G and F time per iteration, model time, total and speed-up against fine_t (or the
+        cached serial fine solve); with F_t, the total is modelled as F_t*K + model time."""
+        sep, beg, end = (' | ', '|', '|') if md else (' & ', '', '\\\\')
+        Fh, Gh = ('F', 'G') if md else ('$T_{\\f}$', '$T_{\\g}$')
+        if F_t is not None:
+            fine_t = F_t * self.N
+        if fine_t is None:
+            fine_t = self.fine_t if self.fine is not None else None
+        if fine_t is None:
+            raise Exception('Running time of fine solver unknown/not provided')
+        names = {'GP': 'GParareal', 'NNGP': 'NN-GParareal'}
+        tab = [['Model', 'K', Gh, Fh, 'Model', 'Total', 'Speed-up'],
+               ['---'] * 7 if md else ['\\hline'],
+               ['Fine', '-', '-', '-', '-', f'{fine_t:.2e}', '1']]
+        for key, label in (mdls if mdls is not None else {k: k for k in self.runs}).items():
+            if key not in self.runs:
+                raise Exception('Unknown model', key)
+            r = self.runs[key]
+            tm = r['timings']
+            total = F_t * r['k'] + tm['mdl_tot_t'] if F_t is not None else tm['runtime']
+            tab.append([names.get(label, label), str(r['k']), f'{tm["G_time"] / r["k"]:.2e}',
+                        f'{tm["F_time"] / r["k"]:.2e}', f'{tm["mdl_tot_t"]:.2e}', f'{tm["runtime"]:.2e}',
+                        f'{fine_t / total:.2f}'])
+        lines = [beg + sep.join(r) + end for r in tab]
+        if md:
+            lines = [f'$N={self.N}$\n'] + lines
+        else:
+            lines = ([r'\caption*{' + mdl_title + r', $N=' + f'{self.N}' + r'$}', r'\begin{tabular}{lcccccc}']
+                     + lines + [r'\end{tabular}\\    \bigskip' + '\n'])
+        out = '\n'.join(lines)
+        print(out)
+        return out
+
     # ------------------------------------------------------------------------------ F sweep
     def _fine_sweep(self, torch, t_dev, Uk, UF, I, N, n):
         """uF[I+1:N+1] = F(u[I:N]) -- sharded over ranks when a process group is active."""

@@ -137,3 +137,21 @@ def test_gp_fit_selection_semantics():
     assert np.isinf(_select_fit(th, f, jit)[1])
     f = np.array([np.nan, -5.0, -6.0] + [0.0] * 6)                     # NaN first: kept (min semantics)
     assert _select_fit(th, f, jit)[2] == -20.0
+
+
+def test_report_tables_layout():
+    """print_times / print_speedup (parareal.py:636-758) on recorded run timings (host only)."""
+    import nngp_amd as g
+    p = g.Parareal.__new__(g.Parareal)
+    p.N = 32
+    p.runs = {'NNGP': {'k': 19, 'timings': {'G_time': 0.01, 'F_time': 0.05, 'mdl_train_t': 0.0, 'mdl_pred_t': 0.2,
+                                            'mdl_tot_t': 0.2, 'runtime': 0.3}}}
+    p.fine, p.fine_t = object(), 2.0
+    t = p.print_times(expected_fine=3.0).split('\n')
+    assert t[0].startswith('|Model|K |') and t[0].rstrip().endswith('E[Speedup]|')
+    assert '6.67' in t[3] and '1.51' in t[3]          # 2.0/0.3 and 3/(3/32*19 + 0.2)
+    s = p.print_speedup(fine_t=1.5).split('\n')
+    assert s[0] == '$N=32$' and s[-1] == '|NN-GParareal | 19 | 5.26e-04 | 2.63e-03 | 2.00e-01 | 3.00e-01 | 5.00|'
+    x = p.print_speedup(F_t=0.1, md=False, mdl_title='Lorenz').split('\n')
+    assert x[0] == r'\caption*{Lorenz, $N=32$}' and x[3] == r'\hline\\'
+    assert x[-3].endswith('& ' + f'{3.2 / (0.1 * 19 + 0.2):.2f}' + r'\\')
