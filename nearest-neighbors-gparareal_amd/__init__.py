@@ -5,7 +5,7 @@ from . import _lib, legacy
 from ._lib import NNGPError, build, lib
 from .configs import Config
 from .models import BareParareal, GPjax_p, ModelAbstr, NNGP_p
-from .parareal import GpuPool, MyPool, Parareal
+from .parareal import GpuPool, MyPool, Parareal, PararealLight
 from .solver import SolverAbstr, SolverRK
 from .systems import (ODE, Brusselator, Burgers, DblPend, FHN_ODE, FHN_PDE, Hopf, Lorenz, Rossler,
                       ThomasLabyrinth, VectorField)

@@ -70,6 +70,22 @@ class _Events:
         return out
 
 
+class _Ring:
+    """Two-column stand-in for the [N+1][n][K] iterate history: PararealLight keeps only the
+    current and next iterates (parareal.py:851-862), so u[..., k] addresses column k % 2."""
+
+    def __init__(self, rows, n):
+        self.a = np.full((rows, n, 2), np.nan)
+
+    def __getitem__(self, key):
+        i, j, k = key
+        return self.a[i, j, k % 2]
+
+    def __setitem__(self, key, v):
+        i, j, k = key
+        self.a[i, j, k % 2] = v
+
+
 def shard_bounds(I, N, world, rank):
     """Contiguous block of the unconverged slices [I, N) owned by `rank`: every
     rank gets ceil((N-I)/world) slices (the last ones fewer or none), so one fixed-size all-gather
@@ -145,6 +161,7 @@ def correction_sweep_sharded(coarse, predict_range, assemble, I, N, U1, UG1, d, 
 
 
 class Parareal():
+    _light = False
 
     def __init__(self, ode, solver, tspan, N, epsilon=5e-7, verbose='v', process_group=None, **kwargs):
         if not isinstance(ode, ODE):
@@ -486,6 +503,15 @@ class Parareal():
     def _parareal(self, model, debug=False, early_stop=None, parall='Serial', store_int=False,
                   _resume=None, **kwargs):
         torch = _lib.require_gpu()
+        light = self._light
+        if light:   # PararealLight (parareal.py:812-1060)
+            if debug:
+                print('WARNING: PararealLight does not support debug mode')
+                debug = False
+            if store_int:
+                raise NotImplementedError('PararealLight does not support storing intermediate results')
+            if kwargs.get('lag_k') is not None or _resume is not None:
+                raise NotImplementedError('PararealLight keeps no per-iteration training history')
         if debug and self.process_group is not None:
             raise NotImplementedError('debug mode runs on one rank')
         one_step_error, all_pred_err = [], []   # debug (parareal.py:258-262)
@@ -504,12 +530,13 @@ class Parareal():
         t_dev = torch.tensor(t, **f64)
         I = 0
         conv_int = []
-        u = np.full((N + 1, n, N + 1), np.nan)
+        u = _Ring(N + 1, n) if light else np.full((N + 1, n, N + 1), np.nan)
         err = np.full((N + 1, N), np.nan)
         x = np.zeros((0, n))
         D = np.zeros((0, n))
-        data_x = np.full((N, n, N), np.nan)
-        data_D = np.full((N, n, N), np.nan)
+        data_x = None if light else np.full((N, n, N), np.nan)
+        data_D = None if light else np.full((N, n, N), np.nan)
+        last = 0   # the column of u holding the newest iterate
         G_time = F_time = F_time_serial = 0.0
 
         u0 = torch.tensor(self.u0, **f64)
@@ -573,8 +600,9 @@ class Parareal():
             d_new = Dd[rows - new:rows].cpu().numpy()
             x = np.vstack([x, u[I - 1:N, :, k]])
             D = np.vstack([D, d_new])
-            data_x[I - 1:N, :, k] = u[I - 1:N, :, k]
-            data_D[I - 1:N, :, k] = d_new
+            if not light:
+                data_x[I - 1:N, :, k] = u[I - 1:N, :, k]
+                data_D[I - 1:N, :, k] = d_new
             fe = ev.collect()
             F_time += fe.get('F', 0.0)
             F_time_serial += fe.get('F', 0.0)   # every slice runs for the whole launch
@@ -584,6 +612,7 @@ class Parareal():
                     print('WARNING: early stopping')
                 u[:, :, k + 1] = Uk1.cpu().numpy()
                 err[:, k] = np.linalg.norm(u[:, :, k + 1] - u[:, :, k], np.inf, 1)
+                last = k if light else k + 1   # PararealLight returns u_curr here
                 err[-1, k] = np.nextafter(epsilon, 0)
                 break
 
@@ -610,6 +639,7 @@ class Parareal():
                                              th0 if is_nngp else None, stream)
             ev.stop(e_loop, 'loop')
             u[:, :, k + 1] = Uk1.cpu().numpy()
+            last = k + 1
             ug = UGk1.cpu().numpy()
             te = ev.collect()
             G_time += g_s
@@ -651,6 +681,28 @@ class Parareal():
         debug_dict = {}
         if debug:   # (:441-463; the reference also plots these)
             debug_dict = {'one_step_error': np.array(one_step_error), 'all_pred_err': all_pred_err}
+        if light:   # (parareal.py:1057-1059): the newest iterate only, no data_x/data_D
+            return {'t': t, 'u': u[:, :, last].copy(), 'err': err[:, :k + 1], 'x': x, 'D': D, 'k': k + 1,
+                    'timings': timings, 'debug_dict': {}, 'converged': I == N, 'conv_int': conv_int}
         return {'t': t, 'u': u[:, :, :k + 1], 'err': err[:, :k + 1], 'x': x, 'D': D, 'k': k + 1,
                 'data_x': data_x[..., :k + 1], 'data_D': data_D[..., :k + 1], 'timings': timings,
                 'debug_dict': debug_dict, 'converged': I == N, 'conv_int': conv_int}
+
+
+class PararealLight(Parareal):
+    """parareal.py:812-1060: the same iteration keeping only the current and next iterates on the
+    host (no [N+1][n][K] history, no per-iteration training arrays); returns the newest iterate
+    as 'u'.  Checkpoints, plots and report tables are not supported, as in the reference."""
+    _light = True
+
+    def load_int_dump(self, *args, **kwargs):
+        raise NotImplementedError('PararealLight does not support loading from intermediate dumps')
+
+    def _run_from_int(self, *args, **kwargs):
+        raise NotImplementedError('PararealLight does not support loading from intermediate dumps')
+
+    def print_times(self, *args, **kwargs):
+        raise NotImplementedError('PararealLight does not support printing times')
+
+    def print_speedup(self, *args, **kwargs):
+        raise NotImplementedError('PararealLight does not support printing speedup')

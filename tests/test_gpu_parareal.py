@@ -165,3 +165,20 @@ def test_debug_mode_reports_prediction_errors_without_changing_the_run(gpu, mode
         assert pe.shape == (32 - I, 3) and np.all(np.isfinite(pe))
         I = b['conv_int'][k] + 1   # the next sweep starts after the next F increment
     assert np.all(dd['one_step_error'][:, 1] == [pe.max() for pe in dd['all_pred_err']])
+
+
+@pytest.mark.parametrize('model', ['nngp', 'gpjax'])
+def test_pararealight_returns_the_newest_iterate(gpu, model):
+    """PararealLight (parareal.py:812-1060): the same iteration with only current/next iterates
+    kept; its 'u' after 3 iterations is column 3 of a Parareal run's history, bit for bit."""
+    ode = gpu.Lorenz(normalization='-11')
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=6, Nf=450, F='RK4', G='RK4')
+    kw = dict(nn=10, seed=45) if model == 'nngp' else {}
+    light = gpu.PararealLight(ode, s, [0, 18], 32, epsilon=5e-7, verbose=None).run(model=model, early_stop=3, **kw)
+    full = gpu.Parareal(ode, s, [0, 18], 32, epsilon=5e-7, verbose=None).run(model=model, early_stop=4, **kw)
+    assert light['u'].shape == (33, 3) and 'data_x' not in light
+    assert np.array_equal(np.nan_to_num(light['u'], nan=7.0), np.nan_to_num(full['u'][:, :, 3], nan=7.0))
+    assert light['conv_int'] == full['conv_int'][:3]
+    assert np.array_equal(light['x'], full['x'][:light['x'].shape[0]])
+    with pytest.raises(NotImplementedError):
+        gpu.PararealLight(ode, s, [0, 18], 32, verbose=None).run(model=model, store_int=True, **kw)
