@@ -29,11 +29,13 @@ sys.path.insert(0, ROOT)
 
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector: half the 157.3 TF FP32 vector peak (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
-# One-wave issue floor of the lane kernel: a slice is one dependent chain, so a
-# step costs (fp64 VALU per step) x (cycles per wave64 fp64 VALU issue).  119 VALU per Hopf RK4
-# step in the gfx950 code object (tools/isa_loop_count.py); 4.22 cycles per independent
-# v_mul/v_add_f64 and a 2.40 GHz shader clock measured on the box (tools/ubench_fp64.hip).
-LANE_VALU_PER_STEP = 119
+# One-wave issue floor of the fine-sweep kernel: a slice is one dependent chain, so
+# a step costs (VALU per step) x (cycles per wave64 VALU issue).  The Hopf sweep at 128 slices runs
+# the lane-group kernel (components across a 16-lane group): 101 VALU per RK4 step in the gfx950
+# code object (tools/isa_loop_count.py rk_group_kernelILi1ELi4ELb0ELb1E; the one-lane-per-slice
+# kernel has 119); 4.22 cycles per independent v_mul/v_add_f64 and a 2.40 GHz shader clock
+# measured on the box (tools/ubench_fp64.hip).
+LANE_VALU_PER_STEP = 101
 CYCLES_PER_F64_VALU = 4.22
 SHADER_GHZ = 2.40
 # algorithmic flops per fine step per slice: S*F_rhs + (2 nnz(a) + S + 2 nnz(b))*d
@@ -316,7 +318,7 @@ def main():
                    'steps_per_slice': args.steps_per_slice, 'parallelism': f'time-slices x{world}'},
         'roofline': {'bound': 'fp64-valu', 'achieved': achieved_tf, 'peak': FP64_PEAK_TFLOPS,
                      'unit': 'TFLOP/s', 'frac': achieved_tf / FP64_PEAK_TFLOPS, 'traffic': read_traffic(),
-                     'kernel': 'rk_lane_kernel<HOPF,RK4>', 'kernel_ms': kernel_s * 1e3,
+                     'kernel': 'rk_group_kernel<HOPF,RK4>', 'kernel_ms': kernel_s * 1e3,
                      'issue_floor_us_per_step': LANE_VALU_PER_STEP * CYCLES_PER_F64_VALU / (SHADER_GHZ * 1e3),
                      'us_per_step': kernel_s / args.steps_per_slice * 1e6,
                      'issue_floor_frac': (LANE_VALU_PER_STEP * CYCLES_PER_F64_VALU / (SHADER_GHZ * 1e9))

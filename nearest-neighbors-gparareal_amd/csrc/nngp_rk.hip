@@ -224,6 +224,130 @@ __global__ void __launch_bounds__(64) rk_lane_kernel(LaneArgs args, int n_slices
 }
 
 // ---------------------------------------------------------------------------------------------
+// Lane-group kernel: one slice = one group of G lanes (G = 16 for the broadcast-coupled fields,
+// 4 for Thomas labyrinth), lane c owns component c (d <= 3, lanes c >= d are padding).
+// The lane kernel above runs every component's stage sums, (de)normalisation, h*k and final update
+// in one lane; here each of those is one instruction per step-part for all components at once, and
+// only the RHS coupling crosses lanes: `v_mov_b64_dpp row_newbcast:c` (gfx950's 64-bit DPP, one
+// VALU op) for G = 16, or a quad_perm rotation (two 32-bit DPP ops) for G = 4.
+// At few slices the step is one wave's instruction issue (a wave with 1 active
+// lane costs the same as 64), so fewer instructions per step is the whole gain, measured on the
+// box (tools/lane_group_probe.py): Hopf RK4 119 -> 101 VALU, 0.250 -> 0.207 us/step; Lorenz
+// 0.29 -> 0.21; Thomas labyrinth one sin per lane instead of three, 1.45 -> 0.52 us/step.
+// Bitwise the lane kernel: each component is rounded by the same expression in the same order.
+// ---------------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double quad_mov(double v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+constexpr int QROT = 0xC9;   // quad_perm [1,2,0,3]: lane c reads lane c+1 mod 3
+
+// broadcast lane L of the slice's lane group: G = 16 -> `v_mov_b64_dpp row_newbcast:L` (gfx950's
+// 64-bit DPP, one op); G = 4 -> quad_perm [L,L,L,L] (32-bit DPP only: two ops)
+template <int G, int L>
+__device__ __forceinline__ double grp_bcast(double v) {
+    if constexpr (G == 16) return __builtin_amdgcn_mov_dpp(v, 0x150 + L, 0xF, 0xF, false);
+    else return __builtin_amdgcn_mov_dpp(v, L * 0x55, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ double sel3(int c, double a, double b, double d) {
+    return c == 0 ? a : (c == 1 ? b : d);
+}
+
+// f<G>(x = own de-normalised component, c) -> own component of f; G = lanes per slice (4 or 16).
+// G16 is the form for the broadcast-coupled fields (Lorenz, Hopf, Rossler: row_newbcast is one
+// 64-bit op), G4 for Thomas labyrinth's rotation (quad_perm).
+template <int SYS> struct GroupSys;
+
+template <> struct GroupSys<NNGP_SYS_LORENZ> {   // systems.py:232-238, as LaneSys<LORENZ>
+    static constexpr int G = 16;
+    template <int GG>
+    __device__ static double f(double x, int c, const LaneArgs &) {
+        const double A = grp_bcast<GG, 0>(x), B = grp_bcast<GG, 1>(x), C = grp_bcast<GG, 2>(x);
+        const double o0 = 10 * (B - A);
+        const double o1 = (28 * A - B) - A * C;
+        const double o2 = A * B - (8.0 / 3) * C;
+        return sel3(c, o0, o1, o2);
+    }
+};
+template <> struct GroupSys<NNGP_SYS_HOPF> {     // systems.py:148-154, as LaneSys<HOPF>
+    static constexpr int G = 16;
+    template <int GG>
+    __device__ static double f(double x, int c, const LaneArgs &a) {
+        const double A = grp_bcast<GG, 0>(x), B = grp_bcast<GG, 1>(x), C = grp_bcast<GG, 2>(x);
+        const double g = (div_const(C, a.param[0], a.rparam0) - A * A) - B * B;
+        // lane 0: -u1 + u0*g, lane 1: u0 + u1*g (own component times g), lane 2: 1
+        const double o = (c == 0 ? -B : A) + x * g;
+        return c == 2 ? 1.0 : o;
+    }
+};
+template <> struct GroupSys<NNGP_SYS_THOMAS_LABYRINTH> {   // systems.py:257-271
+    static constexpr int G = 4;
+    template <int GG>
+    __device__ static double f(double x, int, const LaneArgs &) {
+        const double sn = quad_mov<QROT>(nn_sin(x));   // sin(u[c+1 mod 3])
+        return -0.5 * x + 10.0 * sn;
+    }
+};
+template <> struct GroupSys<NNGP_SYS_ROSSLER> {  // systems.py:116-125
+    static constexpr int G = 16;
+    template <int GG>
+    __device__ static double f(double x, int c, const LaneArgs &) {
+        const double A = grp_bcast<GG, 0>(x), B = grp_bcast<GG, 1>(x), C = grp_bcast<GG, 2>(x);
+        return sel3(c, -B - C, A + (0.2 * B), 0.2 + C * (A - 5.7));
+    }
+};
+
+template <int SYS> struct has_group { static constexpr bool value = false; };
+template <> struct has_group<NNGP_SYS_LORENZ> { static constexpr bool value = true; };
+template <> struct has_group<NNGP_SYS_HOPF> { static constexpr bool value = true; };
+template <> struct has_group<NNGP_SYS_THOMAS_LABYRINTH> { static constexpr bool value = true; };
+template <> struct has_group<NNGP_SYS_ROSSLER> { static constexpr bool value = true; };
+
+template <int SYS, int ORDER, bool LINSPACE, bool NORM>
+__global__ void __launch_bounds__(64) rk_group_kernel(LaneArgs args, int n_slices,
+                                                     const double *__restrict__ t0,
+                                                     const double *__restrict__ t1, int64_t steps,
+                                                     int64_t gsteps, const int64_t *__restrict__ j0s,
+                                                     const double *__restrict__ u0,
+                                                     double *__restrict__ uF) {
+    using T = Tableau<ORDER>;
+    constexpr int S = T::S;
+    constexpr int D = LaneSys<SYS>::D;
+    static_assert(D <= 3, "group kernel: d <= 3");
+    constexpr int G = GroupSys<SYS>::G;
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = tid / G, c = tid % G;
+    if (i >= n_slices) return;   // group-uniform: the DPP partners of a live lane are live
+    const bool own = c < D;
+    double mn = 0, hw = 0, sc = 0;
+    if constexpr (NORM) {
+        if (own) {
+            mn = args.norm[c];
+            hw = 0.5 * args.norm[D + c];
+            sc = args.norm[2 * D + c];
+        }
+    }
+    double u = own ? u0[(size_t)i * D + c] : 0.0, k[S];
+    const double T0 = t0[i], T1 = t1[i];
+    const double dt = (T1 - T0) / (double)(LINSPACE ? gsteps : steps);
+    const int64_t j0 = j0s ? j0s[i] : 0;
+    for (int64_t n = 0; n < steps; n++) {
+        const double h = step_size(LINSPACE, n, j0, gsteps, T0, T1, dt);
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+            const double tmp = stage_input<T, 1>(s, u, k, 0);
+            double o;
+            if constexpr (NORM) o = GroupSys<SYS>::template f<G>((tmp + 1) * hw + mn, c, args) * sc;
+            else o = GroupSys<SYS>::template f<G>(tmp, c, args);
+            k[s] = h * o;
+        }
+        u = step_update<T, 1>(u, k, 0);
+    }
+    if (own) uF[(size_t)i * D + c] = u;
+}
+
+// ---------------------------------------------------------------------------------------------
 // PDE right-hand sides (Burgers, FHN-PDE), one workgroup = one slice
 // ---------------------------------------------------------------------------------------------
 struct FieldArgs {
@@ -535,6 +659,26 @@ static int launch_lane(const nngp_system *sys, int n, const double *t0, const do
     a.norm = sys->norm;
     NNGP_REQUIRE(!sys->normalized || sys->norm != nullptr, "normalized system needs norm[3d]");
     const int bs = 64;
+    if constexpr (has_group<SYS>::value) {
+        // group kernel while all slices' lane groups fit one wave per SIMD (G*n <= 64 * 1024): there
+        // the step time is one wave's issue and the group form issues fewer instructions per step;
+        // beyond it waves share SIMDs and the lane kernel's G-fold fewer waves win.
+        // NNGP_RK_GROUP=0 forces the lane kernel (A/B tool, tests).
+        const char *ge = getenv("NNGP_RK_GROUP");
+        const int group_on = ge ? atoi(ge) : 1;
+        constexpr int G = GroupSys<SYS>::G;
+        if (group_on && (int64_t)n * G <= 64 * 1024) {
+            const int nb = (int)(((int64_t)G * n + bs - 1) / bs);
+            if (sys->normalized)
+                hipLaunchKernelGGL((rk_group_kernel<SYS, ORDER, LIN, true>), dim3(nb), dim3(bs), 0, st,
+                                   a, n, t0, t1, steps, gsteps, j0, u0, uF);
+            else
+                hipLaunchKernelGGL((rk_group_kernel<SYS, ORDER, LIN, false>), dim3(nb), dim3(bs), 0, st,
+                                   a, n, t0, t1, steps, gsteps, j0, u0, uF);
+            NNGP_LAUNCH_CHECK();
+            return NNGP_OK;
+        }
+    }
     if (sys->normalized)
         hipLaunchKernelGGL((rk_lane_kernel<SYS, ORDER, LIN, true>), dim3((n + bs - 1) / bs), dim3(bs), 0, st,
                            a, n, t0, t1, steps, gsteps, j0, u0, uF);

@@ -64,6 +64,29 @@ def test_rk_batch_vs_oracle(gpu, key, tab, mode):
     assert np.max(np.abs(one - ref)) <= tol
 
 
+@pytest.mark.parametrize('key', ['lorenz', 'lorenz_id', 'hopf', 'tomlab', 'rossler'])
+@pytest.mark.parametrize('n', [1, 5, 37, 300, 5000])
+def test_rk_group_kernel_equals_lane_kernel(gpu, key, n, monkeypatch):
+    """The lane-group kernel (one slice per 4- or 16-lane group, components across lanes) is
+    bitwise the one-lane-per-slice kernel, for partial and full waves and past its size limit
+    (n=5000 at 16 lanes per slice falls back to the lane kernel)."""
+    import torch
+    ode = product_ode(gpu, key)
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=7, Nf=200, F='RK4', G='RK4')
+    rng = np.random.default_rng(n)
+    lo, hi = (-0.9, 0.9) if key != 'lorenz_id' else (-15.0, 15.0)
+    U0 = rng.uniform(lo, hi, (n, 3))
+    T0 = rng.uniform(0, 1, n)
+    T1 = T0 + 0.5
+    args = (_t(torch, T0), _t(torch, T1), _t(torch, U0))
+    monkeypatch.setenv('NNGP_RK_GROUP', '1')
+    grp = s.run_F_batch(*args).cpu().numpy()
+    monkeypatch.setenv('NNGP_RK_GROUP', '0')
+    lane = s.run_F_batch(*args).cpu().numpy()
+    assert np.array_equal(grp, lane, equal_nan=True)
+    assert np.all(np.isfinite(grp))
+
+
 def test_rk_batch_uF_may_alias_u0(gpu):
     import torch
     ode = gpu.Burgers(d_x=128, normalization='-11')

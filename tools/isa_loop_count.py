@@ -1,7 +1,7 @@
 """Count the instructions of a kernel's innermost step loop in the gfx950 assembly (for the issue
 floor in DESIGN.md §3.1 / bench.py).  Usage:
 
-    python tools/isa_loop_count.py [kernel-substring]   # default: Hopf RK4 fixed-dt normalised lane kernel
+    python tools/isa_loop_count.py [kernel-substring]   # default: Hopf RK4 fixed-dt normalised lane-group kernel
 """
 import collections
 import os
@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, 'nearest-neighbors-gparareal_amd', 'csrc', 'nngp_rk.hip')
 
 
-def loop_histogram(kernel='rk_lane_kernelILi1ELi4ELb0ELb1E', src=SRC):
+def loop_histogram(kernel='rk_group_kernelILi1ELi4ELb0ELb1E', src=SRC):
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, 'k.s')
         subprocess.run(['/opt/rocm/bin/hipcc', '-O3', '--offload-arch=gfx950', '-std=c++17', '-ffp-contract=off',

@@ -20,7 +20,7 @@ def values(path, sub):
 
 def main():
     fetch, write, out = sys.argv[1:4]
-    sub = sys.argv[4] if len(sys.argv) > 4 else 'rk_lane_kernel'
+    sub = sys.argv[4] if len(sys.argv) > 4 else 'rk_group_kernel'
     f, w = values(fetch, sub), values(write, sub)
     f_warm = f[1:] if len(f) > 1 else f
     w_warm = w[1:] if len(w) > 1 else w
