@@ -277,6 +277,40 @@ def burgers_published_schedule(torch, g, sample_pages=2):
             'us_per_step': per_page / 39999 * 1e6}
 
 
+def tomlab_published_schedule(torch, g, sample_steps=1_000_000):
+    """The published Thomas labyrinth N=256 scalability run (TomLab.py:83-101: Nf = Ng*ceil(1e9/Ng),
+    RK4, RK_thresh = Nf/N/109) pages every slice into 110 pages of the full per-slice count
+    (new_lib.py:57-69): 4.30e8 RK4 steps per slice per iteration.  Time
+    `sample_steps` of them for all 256 slices (LINSPACE grid, lane-group kernel) and scale to the
+    iteration; the reference's F time per iteration on 282 cores was 156 s.  Each
+    slice is one serial chain, so this is per-step latency: a CPU core's 0.30-0.37 us/step vs one
+    GPU lane group's, with all 256 slices on one GPU instead of 282 cores."""
+    ode = g.ThomasLabyrinth(normalization='-11')
+    solver = g.SolverRK(ode.get_vector_field(), Ng=10, Nf=sample_steps, F='RK4', G='RK1',
+                        step_mode='linspace', thresh=float('inf'))
+    n = 256
+    t = np.linspace(0, 100, n + 1)
+    dev = lambda a: torch.tensor(a, dtype=torch.float64, device='cuda')
+    rng = np.random.default_rng(0)
+    U = dev(rng.uniform(-0.5, 0.5, (n, 3)))
+    out = torch.empty_like(U)
+    small = g.SolverRK(ode.get_vector_field(), Ng=10, Nf=1000, F='RK4', G='RK1', step_mode='linspace',
+                       thresh=float('inf'))
+    small.run_F_batch(dev(t[:-1]), dev(t[1:]), U, out=out)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    solver.run_F_batch(dev(t[:-1]), dev(t[1:]), U, out=out)
+    b.record()
+    torch.cuda.synchronize()
+    us = a.elapsed_time(b) * 1e3 / sample_steps
+    eff = 4.30e8
+    it = us * 1e-6 * eff
+    return {'us_per_step': us, 'F_per_iteration_s': it, 'reference_F_per_iteration_s': 156.0,
+            'reference_cores': 282, 'speedup_vs_reference_F': 156.0 / it, 'steps_per_slice': eff,
+            'sample': f'{sample_steps} of 4.30e8 steps x 256 slices, RK4, linspace'}
+
+
 def read_traffic():
     path = os.path.join(ROOT, 'profiles', 'fine_kernel_traffic.json')
     if os.path.exists(path):
@@ -342,6 +376,7 @@ def main():
         res['gparareal_lorenz_n32'] = gparareal_lorenz(torch, g)
         log('gparareal lorenz K', res['gparareal_lorenz_n32']['K'], f"{res['gparareal_lorenz_n32']['wall_s']:.2f}s")
         res['burgers_n128_published_schedule'] = burgers_published_schedule(torch, g)
+        res['tomlab_n256_published_schedule'] = tomlab_published_schedule(torch, g)
         res['cpu_baseline'] = cpu_baseline(args.steps_per_slice, args.slices_per_gpu)
         # north-star target (>= 10x the CPU path on Burgers N=128, identical K): time the first
         # iteration on both sides and extrapolate the CPU to the GPU run's K
