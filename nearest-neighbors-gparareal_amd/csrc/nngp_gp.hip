@@ -1129,9 +1129,13 @@ static int run_nm_spec(NMArgs &a, hipStream_t st, int nq = 1) {
     return NNGP_OK;
 }
 
-// Speculative (a wave per fit) while the fits fit ~2 waves per SIMD; beyond that the packed
-// kernel (4 fits per wave) has the better throughput.  NNGP_NM_SPEC=0/1 forces either (tuning).
-static bool use_spec(int n_fits) {
+// Speculative (a wave per fit) while the fits fit ~2 waves per SIMD (MAXM <= 16) or ~1 (MAXM 24/32,
+// two K rows per lane: twice the VGPRs and issue per evaluation); beyond that the packed kernel
+// (4 fits per wave) has the better throughput.  Crossover measured on the box with
+// `tools/nm_probe.py sweep` (profiles/r01/nm_sweep.txt): m=15 spec wins to 1728 fits, loses at
+// 2304; m=20 spec wins at 864 fits (0.67 vs 0.98 ms), loses from 1152 (1.10 vs 0.98 ms).
+// NNGP_NM_SPEC=0/1 forces either (tuning).
+static bool use_spec(int n_fits, int m) {
     static int forced = -2;
     if (forced == -2) {
         const char *e = getenv("NNGP_NM_SPEC");
@@ -1141,7 +1145,7 @@ static bool use_spec(int n_fits) {
     static int ncu = 0;
     if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) ncu = 256;
     if (ncu <= 0) ncu = 256;
-    return n_fits <= 8 * ncu;
+    return n_fits <= (maxm_for(m) <= 16 ? 8 : 4) * ncu;
 }
 
 // fits per 16-lane group in the unfused kernel's work-queue mode (NNGP_NM_REFILL; 0/1 = off)
@@ -1254,7 +1258,7 @@ extern "C" int nngp_nm_fit_batch(int m, int d, const double *xm, const double *y
     a.coord = coord; a.jitter_idx = jitter_idx; a.theta0 = theta0;
     a.fatol = fatol; a.xatol = xatol; a.maxfev = maxfev; a.R = 1;
     a.theta_out = theta_out; a.fval_out = fval_out; a.nfev_out = nfev_out;
-    if (use_spec(n_fits)) return run_nm_spec(a, st);
+    if (use_spec(n_fits, m)) return run_nm_spec(a, st);
     return run_nm(a, false, st);
 }
 
@@ -1340,7 +1344,7 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
         a.fits_alt = spec_fits;
         a.fits_alt2 = spec2_fits;
     }
-    if (use_spec(a.n_fits)) {   // fits (a wave each), then arg-min + mean (+ bias) per coordinate
+    if (use_spec(a.n_fits, a.m)) {   // fits (a wave each), then arg-min + mean (+ bias) per coordinate
         rc = run_nm_spec(a, st);
         if (rc) return rc;
         return run_mean(a, st);

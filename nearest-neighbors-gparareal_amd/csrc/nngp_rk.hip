@@ -242,59 +242,62 @@ __device__ __forceinline__ double quad_mov(double v) {
 }
 constexpr int QROT = 0xC9;   // quad_perm [1,2,0,3]: lane c reads lane c+1 mod 3
 
-// broadcast lane L of the slice's lane group: G = 16 -> `v_mov_b64_dpp row_newbcast:L` (gfx950's
-// 64-bit DPP, one op); G = 4 -> quad_perm [L,L,L,L] (32-bit DPP only: two ops)
-template <int G, int L>
-__device__ __forceinline__ double grp_bcast(double v) {
-    if constexpr (G == 16) return __builtin_amdgcn_mov_dpp(v, 0x150 + L, 0xF, 0xF, false);
-    else return __builtin_amdgcn_mov_dpp(v, L * 0x55, 0xF, 0xF, false);
+// G = 16: component c lives in DPP bank c (lanes 4c..4c+3 of the row hold the same value; lane 4c
+// writes it), so every cross-lane step is one 64-bit `v_mov_b64_dpp row_newbcast` -- the only DPP
+// control gfx950 allows on 64-bit operands:
+//   bcast<c>(v)            component c's value in every lane;
+//   take<L, BANKS>(o, v)   lanes of the banks in BANKS take lane L's v, the others keep o -- a
+//                          per-component select in one op (bank_mask), where a 64-bit v_cndmask
+//                          is two.
+template <int C>
+__device__ __forceinline__ double bcast(double v) {
+    return __builtin_amdgcn_mov_dpp(v, 0x150 + 4 * C, 0xF, 0xF, false);
+}
+template <int L, int BANKS>
+__device__ __forceinline__ double take(double old, double v) {
+    return __builtin_amdgcn_update_dpp(old, v, 0x150 + L, 0xF, BANKS, false);
 }
 
-__device__ __forceinline__ double sel3(int c, double a, double b, double d) {
-    return c == 0 ? a : (c == 1 ? b : d);
-}
-
-// f<G>(x = own de-normalised component, c) -> own component of f; G = lanes per slice (4 or 16).
-// G16 is the form for the broadcast-coupled fields (Lorenz, Hopf, Rossler: row_newbcast is one
-// 64-bit op), G4 for Thomas labyrinth's rotation (quad_perm).
+// f(x = own de-normalised component, c = its index, one = 1.0) -> own component of f.  G16 (bank layout above)
+// for the broadcast-coupled fields (Lorenz, Hopf, Rossler), G4 (lane c = component c) for Thomas
+// labyrinth's rotation (quad_perm, two 32-bit DPP ops).
 template <int SYS> struct GroupSys;
 
 template <> struct GroupSys<NNGP_SYS_LORENZ> {   // systems.py:232-238, as LaneSys<LORENZ>
     static constexpr int G = 16;
-    template <int GG>
-    __device__ static double f(double x, int c, const LaneArgs &) {
-        const double A = grp_bcast<GG, 0>(x), B = grp_bcast<GG, 1>(x), C = grp_bcast<GG, 2>(x);
+    __device__ static double f(double x, int, double, const LaneArgs &) {
+        const double A = bcast<0>(x), B = bcast<1>(x), C = bcast<2>(x);
         const double o0 = 10 * (B - A);
         const double o1 = (28 * A - B) - A * C;
         const double o2 = A * B - (8.0 / 3) * C;
-        return sel3(c, o0, o1, o2);
+        return take<8, 0x4>(take<4, 0x2>(o0, o1), o2);
     }
 };
 template <> struct GroupSys<NNGP_SYS_HOPF> {     // systems.py:148-154, as LaneSys<HOPF>
     static constexpr int G = 16;
-    template <int GG>
-    __device__ static double f(double x, int c, const LaneArgs &a) {
-        const double A = grp_bcast<GG, 0>(x), B = grp_bcast<GG, 1>(x), C = grp_bcast<GG, 2>(x);
+    __device__ static double f(double x, int c, double one, const LaneArgs &a) {
+        const double A = bcast<0>(x), B = bcast<1>(x), C = bcast<2>(x);
         const double g = (div_const(C, a.param[0], a.rparam0) - A * A) - B * B;
-        // lane 0: -u1 + u0*g, lane 1: u0 + u1*g (own component times g), lane 2: 1
-        const double o = (c == 0 ? -B : A) + x * g;
-        return c == 2 ? 1.0 : o;
+        // component 0: -u1 + u0*g, component 1: u0 + u1*g (own component times g), component 2: 1.
+        // p by v_cndmask: a take<4, 0x1>(A, -x) would read -x right after the VALU writing it (DPP
+        // hazard wait states) and copy A into its destination first -- measured slower (0.215 vs
+        // 0.208 us/step); the constant `one` has neither cost.
+        const double p = c == 0 ? -B : A;
+        return take<8, 0x4>(p + x * g, one);
     }
 };
 template <> struct GroupSys<NNGP_SYS_THOMAS_LABYRINTH> {   // systems.py:257-271
     static constexpr int G = 4;
-    template <int GG>
-    __device__ static double f(double x, int, const LaneArgs &) {
+    __device__ static double f(double x, int, double, const LaneArgs &) {
         const double sn = quad_mov<QROT>(nn_sin(x));   // sin(u[c+1 mod 3])
         return -0.5 * x + 10.0 * sn;
     }
 };
 template <> struct GroupSys<NNGP_SYS_ROSSLER> {  // systems.py:116-125
     static constexpr int G = 16;
-    template <int GG>
-    __device__ static double f(double x, int c, const LaneArgs &) {
-        const double A = grp_bcast<GG, 0>(x), B = grp_bcast<GG, 1>(x), C = grp_bcast<GG, 2>(x);
-        return sel3(c, -B - C, A + (0.2 * B), 0.2 + C * (A - 5.7));
+    __device__ static double f(double x, int, double, const LaneArgs &) {
+        const double A = bcast<0>(x), B = bcast<1>(x), C = bcast<2>(x);
+        return take<8, 0x4>(take<4, 0x2>(-B - C, A + (0.2 * B)), 0.2 + C * (A - 5.7));
     }
 };
 
@@ -317,9 +320,11 @@ __global__ void __launch_bounds__(64) rk_group_kernel(LaneArgs args, int n_slice
     static_assert(D <= 3, "group kernel: d <= 3");
     constexpr int G = GroupSys<SYS>::G;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const int i = tid / G, c = tid % G;
+    const int i = tid / G, c = (G == 16) ? (tid % 16) >> 2 : tid % G;   // component of this lane
     if (i >= n_slices) return;   // group-uniform: the DPP partners of a live lane are live
     const bool own = c < D;
+    const bool writer = own && (G != 16 || (tid & 3) == 0);
+    const double one = 1.0;
     double mn = 0, hw = 0, sc = 0;
     if constexpr (NORM) {
         if (own) {
@@ -338,13 +343,13 @@ __global__ void __launch_bounds__(64) rk_group_kernel(LaneArgs args, int n_slice
         for (int s = 0; s < S; s++) {
             const double tmp = stage_input<T, 1>(s, u, k, 0);
             double o;
-            if constexpr (NORM) o = GroupSys<SYS>::template f<G>((tmp + 1) * hw + mn, c, args) * sc;
-            else o = GroupSys<SYS>::template f<G>(tmp, c, args);
+            if constexpr (NORM) o = GroupSys<SYS>::f((tmp + 1) * hw + mn, c, one, args) * sc;
+            else o = GroupSys<SYS>::f(tmp, c, one, args);
             k[s] = h * o;
         }
         u = step_update<T, 1>(u, k, 0);
     }
-    if (own) uF[(size_t)i * D + c] = u;
+    if (writer) uF[(size_t)i * D + c] = u;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -42,6 +42,13 @@ def case(d, m, R, rows, seed=0):
 
 if __name__ == '__main__':
     torch.cuda.set_device(0)
+    if len(sys.argv) > 1 and sys.argv[1] == 'sweep':
+        # spec-vs-packed crossover (run once with NNGP_NM_SPEC=1 and once with 0)
+        for m, ds in ((15, (64, 96, 128, 160, 192, 256)), (20, (32, 64, 96, 128, 160, 200)),
+                      (30, (16, 32, 64, 96))):
+            for d in ds:
+                case(d, m, 1, 1500)
+        sys.exit(0)
     case(3, 15, 2, 600)
     case(3, 10, 1, 600)
     case(128, 15, 1, 1200)
