@@ -301,11 +301,51 @@ template <> struct GroupSys<NNGP_SYS_ROSSLER> {  // systems.py:116-125
     }
 };
 
+template <> struct GroupSys<NNGP_SYS_FHN_ODE> {  // systems.py:87-95, as LaneSys<FHN_ODE>
+    static constexpr int G = 16;
+    __device__ static double f(double x, int, double, const LaneArgs &) {
+        const double A = bcast<0>(x), B = bcast<1>(x);
+        const double c = 3;
+        const double o0 = c * ((A - div_const(A * (A * A), 3.0, 1.0 / 3)) + B);
+        const double o1 = -(1 / c) * ((A - 0.2) + 0.2 * B);
+        return take<4, 0x2>(o0, o1);
+    }
+};
+template <> struct GroupSys<NNGP_SYS_BRUSSELATOR> {  // systems.py:209-214, as LaneSys<BRUSSELATOR>
+    static constexpr int G = 16;
+    __device__ static double f(double x, int, double, const LaneArgs &) {
+        const double A = bcast<0>(x), B = bcast<1>(x);
+        const double o0 = (1 + (A * A) * B) - (3 + 1) * A;
+        const double o1 = 3 * A - (A * A) * B;
+        return take<4, 0x2>(o0, o1);
+    }
+};
+template <> struct GroupSys<NNGP_SYS_DBL_PEND> {  // systems.py:182-189, as LaneSys<DBL_PEND>
+    static constexpr int G = 16;
+    __device__ static double f(double x, int, double, const LaneArgs &) {
+        const double A = bcast<0>(x), B = bcast<1>(x), C = bcast<2>(x), D = bcast<3>(x);
+        // the lane kernel's three sincos (of u0-u2, u0, u2) as one per bank: bank 0 takes u0-u2,
+        // bank 1 u0 (lane 0's x), bank 2 u2 (lane 8's x)
+        const double arg = take<8, 0x4>(take<0, 0x2>(A - C, x), x);
+        double sn, cs;
+        nn_sincos(arg, sn, cs);
+        const double s = bcast<0>(sn), c = bcast<0>(cs), s0 = bcast<1>(sn), s2 = bcast<2>(sn);
+        const double pre = -1 / (2 - c * c);
+        const double o1 = pre * ((((B * B) * c) * s + (D * D) * s) + 2 * s0 - c * s2);
+        const double o3 = pre * ((((-2 * (B * B)) * s - ((D * D) * s) * c) - (2 * c) * s0) + 2 * s2);
+        // component 0: u1, 1: o1, 2: u3 (lane 12's x), 3: o3
+        return take<12, 0x8>(take<12, 0x4>(take<4, 0x2>(B, o1), x), o3);
+    }
+};
+
 template <int SYS> struct has_group { static constexpr bool value = false; };
 template <> struct has_group<NNGP_SYS_LORENZ> { static constexpr bool value = true; };
 template <> struct has_group<NNGP_SYS_HOPF> { static constexpr bool value = true; };
 template <> struct has_group<NNGP_SYS_THOMAS_LABYRINTH> { static constexpr bool value = true; };
 template <> struct has_group<NNGP_SYS_ROSSLER> { static constexpr bool value = true; };
+template <> struct has_group<NNGP_SYS_FHN_ODE> { static constexpr bool value = true; };
+template <> struct has_group<NNGP_SYS_BRUSSELATOR> { static constexpr bool value = true; };
+template <> struct has_group<NNGP_SYS_DBL_PEND> { static constexpr bool value = true; };
 
 template <int SYS, int ORDER, bool LINSPACE, bool NORM>
 __global__ void __launch_bounds__(64) rk_group_kernel(LaneArgs args, int n_slices,
@@ -317,7 +357,7 @@ __global__ void __launch_bounds__(64) rk_group_kernel(LaneArgs args, int n_slice
     using T = Tableau<ORDER>;
     constexpr int S = T::S;
     constexpr int D = LaneSys<SYS>::D;
-    static_assert(D <= 3, "group kernel: d <= 3");
+    static_assert(D <= (GroupSys<SYS>::G == 16 ? 4 : 3), "group kernel: one DPP bank (G=16) or lane (G=4) per component");
     constexpr int G = GroupSys<SYS>::G;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
     const int i = tid / G, c = (G == 16) ? (tid % 16) >> 2 : tid % G;   // component of this lane

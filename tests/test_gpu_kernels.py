@@ -64,18 +64,18 @@ def test_rk_batch_vs_oracle(gpu, key, tab, mode):
     assert np.max(np.abs(one - ref)) <= tol
 
 
-@pytest.mark.parametrize('key', ['lorenz', 'lorenz_id', 'hopf', 'tomlab', 'rossler'])
+@pytest.mark.parametrize('key', ['lorenz', 'lorenz_id', 'hopf', 'tomlab', 'rossler', 'fhn_ode', 'brus', 'dblpend'])
 @pytest.mark.parametrize('n', [1, 5, 37, 300, 5000])
 def test_rk_group_kernel_equals_lane_kernel(gpu, key, n, monkeypatch):
     """The lane-group kernel (one slice per 4- or 16-lane group, components across lanes) is
     bitwise the one-lane-per-slice kernel, for partial and full waves and past its size limit
-    (n=5000 at 16 lanes per slice falls back to the lane kernel)."""
+    (n=5000 at 16 lanes per slice falls back to the lane kernel); d = 2, 3 and 4."""
     import torch
     ode = product_ode(gpu, key)
     s = gpu.SolverRK(ode.get_vector_field(), Ng=7, Nf=200, F='RK4', G='RK4')
     rng = np.random.default_rng(n)
     lo, hi = (-0.9, 0.9) if key != 'lorenz_id' else (-15.0, 15.0)
-    U0 = rng.uniform(lo, hi, (n, 3))
+    U0 = rng.uniform(lo, hi, (n, len(ode.get_init_cond())))
     T0 = rng.uniform(0, 1, n)
     T1 = T0 + 0.5
     args = (_t(torch, T0), _t(torch, T1), _t(torch, U0))

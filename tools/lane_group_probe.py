@@ -19,7 +19,7 @@ def run(ode, n, steps, quad):
     s = nngp_amd.SolverRK(ode.get_vector_field(), Ng=4, Nf=steps, F='RK4', G='RK1')
     rng = np.random.default_rng(0)
     dev = lambda a: torch.tensor(a, dtype=torch.float64, device='cuda')
-    U0 = dev(rng.uniform(-0.5, 0.5, (n, 3)))
+    U0 = dev(rng.uniform(-0.5, 0.5, (n, len(ode.get_init_cond()))))
     T0 = dev(np.linspace(0, 1, n))
     T1 = T0 + 1e-3
     s.run_F_batch(T0, T1, U0)
@@ -38,7 +38,10 @@ def main():
     for name, ode, ns in [('hopf', nngp_amd.Hopf(normalization='-11'), (128, 1024)),
                           ('lorenz', nngp_amd.Lorenz(normalization='-11'), (32, 128)),
                           ('tomlab', nngp_amd.ThomasLabyrinth(normalization='-11'), (32, 256)),
-                          ('rossler', nngp_amd.Rossler(normalization='-11'), (128,))]:
+                          ('rossler', nngp_amd.Rossler(normalization='-11'), (128,)),
+                          ('fhn_ode', nngp_amd.FHN_ODE(normalization='-11'), (128,)),
+                          ('brus', nngp_amd.Brusselator(normalization='-11'), (128,)),
+                          ('dblpend', nngp_amd.DblPend(normalization='-11'), (128,))]:
         for n in ns:
             tl, a = run(ode, n, steps, 0)
             tg, b = run(ode, n, steps, 1)
