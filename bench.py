@@ -311,6 +311,47 @@ def tomlab_published_schedule(torch, g, sample_steps=1_000_000):
             'sample': f'{sample_steps} of 4.30e8 steps x 256 slices, RK4, linspace'}
 
 
+def fhn_pde_fine_sweeps(torch, g):
+    """FHN-PDE N=512 fine sweeps on the field kernel (RK8, all 512 slices in one launch):
+    - d=200 (d_x=10) on the published schedule (FHN_PDE.py:146-161, legacy linspace grids, '-11'
+      with +-1 bounds): 5.08e6 effective RK8 steps per slice per iteration; the
+      reference's F per iteration on 517 cores was 202 s (BASELINE.md A);
+    - d=800 (d_x=20), BASELINE configs[4]: 195 325 RK8 steps per slice per iteration (SURVEY.md
+      §8d), with the achieved FP64 rate against the VALU peak (215 600 flops per step per slice).
+    A sample of steps is timed for all 512 slices and scaled to the iteration."""
+    dev = lambda a: torch.tensor(a, dtype=torch.float64, device='cuda')
+    res = {}
+    for nx, mode, norm, sample, eff, ref in ((10, 'linspace', '-11', 10000, 5.08e6, 202.0),
+                                             (20, 'fixed', None, 2000, 195325, None)):
+        ode = g.FHN_PDE(d_x=nx, normalization=norm) if norm else g.FHN_PDE(d_x=nx)
+        n, d = 512, 2 * nx * nx
+        solver = g.SolverRK(ode.get_vector_field(), Ng=1, Nf=sample, F='RK8', G='RK1', step_mode=mode,
+                            thresh=float('inf'))
+        t = np.linspace(0, 1100, n + 1)
+        rng = np.random.default_rng(0)
+        U = dev(np.clip(ode.get_init_cond()[None, :] + 0.01 * rng.standard_normal((n, d)), -1, 1))
+        out = torch.empty_like(U)
+        solver.run_F_batch(dev(t[:-1]), dev(t[1:]), U, out=out)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        solver.run_F_batch(dev(t[:-1]), dev(t[1:]), U, out=out)
+        b.record()
+        torch.cuda.synchronize()
+        sec = a.elapsed_time(b) / 1e3
+        us = sec / sample * 1e6
+        flops = 15.5 * d * 11 + (2 * 39 + 11 + 2 * 5) * d   # SURVEY.md §8d: S*F_rhs + (2nnz(a)+S+2nnz(b))*d
+        tf = n * sample * flops / sec / 1e12
+        r = {'d': d, 'slices': n, 'us_per_step': us, 'steps_per_s': n * sample / sec, 'tflops': tf,
+             'frac_fp64_peak': tf / FP64_PEAK_TFLOPS, 'steps_per_slice_per_iteration': eff,
+             'F_per_iteration_s': us * 1e-6 * eff, 'sample': f'{sample} RK8 steps x 512 slices, {mode}'}
+        if ref:
+            r.update({'reference_F_per_iteration_s': ref, 'reference_cores': 517,
+                      'speedup_vs_reference_F': ref / (us * 1e-6 * eff)})
+        res[f'd{d}'] = r
+    return res
+
+
 def read_traffic():
     path = os.path.join(ROOT, 'profiles', 'fine_kernel_traffic.json')
     if os.path.exists(path):
@@ -377,6 +418,7 @@ def main():
         log('gparareal lorenz K', res['gparareal_lorenz_n32']['K'], f"{res['gparareal_lorenz_n32']['wall_s']:.2f}s")
         res['burgers_n128_published_schedule'] = burgers_published_schedule(torch, g)
         res['tomlab_n256_published_schedule'] = tomlab_published_schedule(torch, g)
+        res['fhn_pde_n512_fine_sweep'] = fhn_pde_fine_sweeps(torch, g)
         res['cpu_baseline'] = cpu_baseline(args.steps_per_slice, args.slices_per_gpu)
         # north-star target (>= 10x the CPU path on Burgers N=128, identical K): time the first
         # iteration on both sides and extrapolate the CPU to the GPU run's K
