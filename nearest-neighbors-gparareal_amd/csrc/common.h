@@ -48,7 +48,7 @@ void set_error(const char *fmt, ...);
 // speculative sweep's batch buffers, which must outlive the per-slice calls.  Growing a slot
 // frees the old buffer after hipFree's implicit device synchronisation.  Not thread-safe across
 // host threads sharing a device.
-constexpr int N_WS_SLOTS = 5;   // slot 2: the sweep's speculation buffers; 3: full-GP factors; 4: fit queues
+constexpr int N_WS_SLOTS = 6;   // slot 2: the sweep's speculation buffers; 3: full-GP factors; 4: fit queues; 5: parked fits
 void *workspace(size_t bytes, int *err, int slot = 0);
 
 int predict_impl(const double *X, const double *Y, int64_t rows, int d, const double *new_x, int m,

@@ -719,6 +719,12 @@ struct NMArgs {
     // unfused fits kernel: per-prediction work queues ([gridDim.y] counters, zeroed) -- a row whose
     // fit is done takes the next unassigned fit, or NULL (one fit per row)
     int32_t *queue;
+    // tail hand-off (single prediction): the packed kernel parks a fit whose evaluation count
+    // reaches park_cap (its Nelder-Mead state, pending request included, in park[f], f appended to
+    // park_list); the speculative kernel then resumes the parked fits (resume != 0), a wave each
+    int park_cap, resume;
+    NM *park;
+    int32_t *park_list, *park_count;
 };
 
 // apply the blockIdx.y prediction offsets of a batched launch (all zero otherwise)
@@ -789,8 +795,10 @@ __global__ void __launch_bounds__(NMBound<MAXM>::T) nm_fit_kernel(NMArgs a) {
     gp_image_init<MAXM>(Kimg, m, l);
     NMCfg cfg{a.fatol, a.xatol, a.maxfev, a.maxfev};
     NM St;
+    bool parked = false;
     // (re)start this row on fit f: its coordinate column, jitter and initial simplex
     auto start_fit = [&]() {
+        parked = false;
         if (!FUSED && valid) {
             if (a.coord) {
                 coord = a.coord[f];
@@ -819,7 +827,7 @@ __global__ void __launch_bounds__(NMBound<MAXM>::T) nm_fit_kernel(NMArgs a) {
     };
     auto write_fit = [&]() {
         const double fval = (St.f1 != St.f1 || St.f2 != St.f2) ? NAN : St.f0;
-        if (valid && l == 0) {
+        if (valid && l == 0 && !parked) {
             if (a.theta_out) { a.theta_out[2 * f] = St.s0x; a.theta_out[2 * f + 1] = St.s0y; }
             if (a.fval_out) a.fval_out[f] = fval;
             if (a.nfev_out) a.nfev_out[f] = St.fcalls;
@@ -856,7 +864,20 @@ __global__ void __launch_bounds__(NMBound<MAXM>::T) nm_fit_kernel(NMArgs a) {
         const bool need = St.st != ST_DONE;
         if (!__any(need)) break;
         const double fv = gp_nlml<MAXM>(m, l, P, sD2, St.px, St.py, jit, y, Kimg);
-        if (need) nm_consume(St, cfg, fv);
+        if (need) {
+            nm_consume(St, cfg, fv);
+            if (!FUSED && a.park_cap && St.st != ST_DONE && St.fcalls >= a.park_cap) {
+                // a long fit: park it (state with its pending request) for the speculative kernel,
+                // which finishes it a wave per fit in ~1.5x fewer rounds, so this wave's tail does
+                // not set the launch's length (uniform within the group)
+                if (l == 0) {
+                    a.park[f] = St;
+                    a.park_list[atomicAdd(a.park_count, 1)] = f;
+                }
+                parked = true;
+                St.st = ST_DONE;
+            }
+        }
     }
     write_fit();
     if constexpr (!FUSED) return;
@@ -934,10 +955,15 @@ __global__ void __launch_bounds__(256) nm_spec_kernel(NMArgs a) {
     const int tid = threadIdx.x;
     const int g = (tid & 63) / 16;                      // row of the wave = candidate slot
     const int l = tid % 16;
-    const int f = blockIdx.x * (blockDim.x / 64) + tid / 64;   // one fit per wave
+    int f = blockIdx.x * (blockDim.x / 64) + tid / 64;   // one fit per wave
     for (int i = tid; i < m * m; i += blockDim.x) sD2[i] = a.D2[i];
     __syncthreads();
-    if (f >= a.n_fits) return;                          // whole wave exits together
+    if (a.resume) {                                      // the parked fits of the packed kernel
+        if (f >= *a.park_count) return;
+        f = a.park_list[f];
+    } else if (f >= a.n_fits) {
+        return;                                          // whole wave exits together
+    }
     int coord, jidx;
     if (a.coord) {
         coord = a.coord[f];
@@ -960,16 +986,20 @@ __global__ void __launch_bounds__(256) nm_spec_kernel(NMArgs a) {
 
     NMCfg cfg{a.fatol, a.xatol, a.maxfev, a.maxfev};
     NM St;
-    St.fcalls = 0;
-    St.iters = 0;
-    St.f0 = St.f1 = St.f2 = INFINITY;
-    St.xbx = St.xby = St.xrx = St.xry = St.fxr = 0.0;
-    const double t0x = a.theta0[2 * f], t0y = a.theta0[2 * f + 1];
-    St.s0x = t0x; St.s0y = t0y;
-    St.s1x = (t0x != 0) ? (1 + 0.05) * t0x : 0.00025; St.s1y = t0y;   // nonzdelt / zdelt
-    St.s2x = t0x; St.s2y = (t0y != 0) ? (1 + 0.05) * t0y : 0.00025;
-    St.st = ST_INIT0;
-    if (!nm_req(St, cfg, St.s0x, St.s0y, ST_INIT0)) St.st = ST_DONE;
+    if (a.resume) {
+        St = a.park[f];   // pending request included: the loop below continues it unchanged
+    } else {
+        St.fcalls = 0;
+        St.iters = 0;
+        St.f0 = St.f1 = St.f2 = INFINITY;
+        St.xbx = St.xby = St.xrx = St.xry = St.fxr = 0.0;
+        const double t0x = a.theta0[2 * f], t0y = a.theta0[2 * f + 1];
+        St.s0x = t0x; St.s0y = t0y;
+        St.s1x = (t0x != 0) ? (1 + 0.05) * t0x : 0.00025; St.s1y = t0y;   // nonzdelt / zdelt
+        St.s2x = t0x; St.s2y = (t0y != 0) ? (1 + 0.05) * t0y : 0.00025;
+        St.st = ST_INIT0;
+        if (!nm_req(St, cfg, St.s0x, St.s0y, ST_INIT0)) St.st = ST_DONE;
+    }
     while (St.st != ST_DONE) {   // wave-uniform
         NMCand c[4];
         const int nc = nm_candidates(St, c);
@@ -1185,6 +1215,13 @@ static int run_nm(NMArgs &a, bool fused, hipStream_t st, int nq = 1) {
         a.cpw = cpw;
         threads = thr(cpw);
         nblocks = (a.d + cpw - 1) / cpw;
+    } else if (a.park_cap && nq == 1) {
+        // one prediction with the tail hand-off: a wave (4 fits) per workgroup so the fits spread
+        // over every CU like the fused kernel's; no work queue -- the long fits are parked instead
+        threads = 64;
+        nblocks = (a.n_fits + 3) / 4;
+        a.cpw = 1;
+        a.queue = nullptr;
     } else {
         threads = 256;
         nblocks = (a.n_fits + threads / 16 - 1) / (threads / 16);
@@ -1207,6 +1244,36 @@ static int run_nm(NMArgs &a, bool fused, hipStream_t st, int nq = 1) {
     case 24: return launch_nm<24>(a, fused, nblocks, threads, lds, st, nq);
     default: return launch_nm<32>(a, fused, nblocks, threads, lds, st, nq);
     }
+}
+
+// evaluation count at which the packed kernel parks a fit for the speculative kernel
+// (NNGP_NM_PARK; 0 = never)
+static int nm_park_cap() {
+    const char *e = getenv("NNGP_NM_PARK");
+    const int v = e ? atoi(e) : 70;
+    return v < 0 ? 0 : v;
+}
+
+// packed fits of ONE prediction with the tail hand-off: fits still running at nm_park_cap()
+// evaluations are parked and finished by the speculative kernel (bitwise the same fits)
+static int run_nm_parked(NMArgs a, hipStream_t st) {
+    const int cap = nm_park_cap();
+    if (cap <= 0) return run_nm(a, false, st);
+    int err = 0;
+    char *ws = (char *)workspace(sizeof(NM) * (size_t)a.n_fits + sizeof(int32_t) * ((size_t)a.n_fits + 1), &err, 5);
+    if (err) return err;
+    NM *park = (NM *)ws;
+    int32_t *cnt = (int32_t *)(park + a.n_fits);
+    NNGP_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int32_t), st));
+    a.park_cap = cap;
+    a.park = park;
+    a.park_count = cnt;
+    a.park_list = cnt + 1;
+    int rc = run_nm(a, false, st);
+    if (rc) return rc;
+    a.park_cap = 0;
+    a.resume = 1;
+    return run_nm_spec(a, st);
 }
 
 }  // namespace nngp
@@ -1259,7 +1326,7 @@ extern "C" int nngp_nm_fit_batch(int m, int d, const double *xm, const double *y
     a.fatol = fatol; a.xatol = xatol; a.maxfev = maxfev; a.R = 1;
     a.theta_out = theta_out; a.fval_out = fval_out; a.nfev_out = nfev_out;
     if (use_spec(n_fits, m)) return run_nm_spec(a, st);
-    return run_nm(a, false, st);
+    return run_nm_parked(a, st);
 }
 
 extern "C" int nngp_gp_mean(int m, int d, const double *xm, const double *ym, const double *new_x,
@@ -1349,17 +1416,17 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
         if (rc) return rc;
         return run_mean(a, st);
     }
-    if (!spec) {
+    if (!spec && nm_park_cap() == 0) {
         NMArgs fu = a;
         fu.fits_out = fits_out;
         rc = run_nm(fu, true, st);
         if (rc != NNGP_E_UNSUPPORTED) return rc;
     }
-    // a coordinate's fits exceed one workgroup (large m with restarts), or speculation: fits
-    // kernel, then the per-coordinate arg-min + posterior mean kernel
+    // the packed fits with the tail hand-off (or: a coordinate's fits exceed one workgroup, or
+    // speculation), then the per-coordinate arg-min + posterior mean kernel
     NMArgs u = a;
     u.preds = nullptr; u.out = nullptr; u.bias = nullptr;
-    rc = run_nm(u, false, st);
+    rc = run_nm_parked(u, st);
     if (rc) return rc;
     return run_mean(a, st);
 }

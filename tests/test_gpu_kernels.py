@@ -245,15 +245,19 @@ def test_predict_restarts_and_small_training_set(gpu):
     assert np.max(np.abs(got - ora)) <= 1e-12 * max(1e-6, np.max(np.abs(ora)))
 
 
+@pytest.mark.parametrize('park', ['0', '30', '100'])
 @pytest.mark.parametrize('m,d,R', [(5, 3, 1), (12, 4, 2), (16, 3, 2), (20, 6, 1), (20, 3, 2), (30, 2, 2),
-                                   (10, 300, 1), (18, 130, 2)])
-def test_predict_every_padded_size_and_fallback_vs_oracle(gpu, m, d, R):
+                                   (10, 300, 1), (18, 130, 2), (20, 80, 1)])
+def test_predict_every_padded_size_and_fallback_vs_oracle(gpu, m, d, R, park, monkeypatch):
     """Fits run padded to 8/16/24/32 rows (identity pad, exact).  Up to 8 fits per CU each fit
     gets a wave and evaluates reflect/expand/contract points speculatively; above that (d=300:
     2 700 fits) the packed kernel runs 4 fits per wave, fused with the arg-min and mean -- or,
     when a coordinate's fits exceed a workgroup (m=18, R=2 at d=130: 4 680 fits), as fits +
-    arg-min/mean kernels.  Every path is bitwise the oracle."""
+    arg-min/mean kernels.  With the tail hand-off (NNGP_NM_PARK = cap > 0) the packed kernel
+    parks every fit still running at `cap` evaluations and the speculative kernel resumes it
+    (cap 30 parks most fits).  Every path is bitwise the oracle."""
     import torch
+    monkeypatch.setenv('NNGP_NM_PARK', park)
     rng = np.random.default_rng(m * 10 + d + R)
     X = np.cumsum(0.05 * rng.standard_normal((3 * m, d)), axis=0)
     Y = 0.01 * np.sin(3 * X) + 1e-5 * rng.standard_normal(X.shape)

@@ -49,6 +49,13 @@ if __name__ == '__main__':
             for d in ds:
                 case(d, m, 1, 1500)
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == 'park':
+        # packed-kernel shapes (run with NNGP_NM_PARK=0 / 60 / 100 / 150)
+        case(256, 15, 1, 1500)
+        case(400, 15, 1, 2000)
+        case(200, 20, 1, 3000)
+        case(800, 20, 1, 4000)
+        sys.exit(0)
     case(3, 15, 2, 600)
     case(3, 10, 1, 600)
     case(128, 15, 1, 1200)
