@@ -826,7 +826,13 @@ static int launch_field(const nngp_system *sys, int n, const double *t0, const d
     }
     const int bt = pick_threads(sys->d, n);
     const int ept = (sys->d + bt - 1) / bt;
-    NNGP_REQUIRE(ept <= 8, "d=%d too large for the field kernel (max 2048)", sys->d);
+    NNGP_REQUIRE(ept <= 8, "d=%d with %d threads per slice exceeds the field kernel's 8 elements per thread",
+                 sys->d, bt);
+    // each EPT variant is compiled for at most 1024 / 512 / 256 / 256 threads (launch bounds): a
+    // larger block (only reachable through NNGP_RK_THREADS) would fail to launch
+    const int bound = ept <= 1 ? 1024 : (ept <= 2 ? 512 : 256);
+    NNGP_REQUIRE(bt <= bound, "%d threads per slice exceed the field kernel's bound %d at %d elements per thread "
+                 "(d=%d)", bt, bound, ept <= 2 ? ept : (ept <= 4 ? 4 : 8), sys->d);
     if (ept <= 1) return launch_field_ept<SYS, ORDER, LIN, 1>(fa, bt, n, t0, t1, steps, gsteps, j0, u0, uF, st);
     if (ept <= 2) return launch_field_ept<SYS, ORDER, LIN, 2>(fa, bt, n, t0, t1, steps, gsteps, j0, u0, uF, st);
     if (ept <= 4) return launch_field_ept<SYS, ORDER, LIN, 4>(fa, bt, n, t0, t1, steps, gsteps, j0, u0, uF, st);

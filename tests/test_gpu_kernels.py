@@ -87,6 +87,30 @@ def test_rk_group_kernel_equals_lane_kernel(gpu, key, n, monkeypatch):
     assert np.all(np.isfinite(grp))
 
 
+@pytest.mark.parametrize('nx', [10, 20])
+def test_field_kernel_thread_overrides(gpu, nx, monkeypatch):
+    """Every valid NNGP_RK_THREADS layout of the field kernel is bitwise the default one; a block
+    larger than the chosen variant's launch bound is refused with an error, not launched."""
+    import torch
+    ode = gpu.FHN_PDE(d_x=nx)
+    d = 2 * nx * nx
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=1, Nf=20, F='RK8', G='RK1')
+    rng = np.random.default_rng(nx)
+    U0 = _t(torch, np.clip(ode.get_init_cond()[None, :] + 0.01 * rng.standard_normal((6, d)), -1, 1))
+    T0 = _t(torch, np.arange(6) * 0.5)
+    T1 = T0 + 0.5
+    ref = s.run_F_batch(T0, T1, U0).cpu().numpy()
+    for thr in (64, 128, 192, 256, 384, 512, 832, 1024):
+        ept = -(-d // thr)
+        ok = ept <= 8 and thr <= (1024 if ept <= 1 else 512 if ept <= 2 else 256)
+        monkeypatch.setenv('NNGP_RK_THREADS', str(thr))
+        if ok:
+            assert np.array_equal(s.run_F_batch(T0, T1, U0).cpu().numpy(), ref), thr
+        else:
+            with pytest.raises(gpu.NNGPError):
+                s.run_F_batch(T0, T1, U0)
+
+
 def test_rk_batch_uF_may_alias_u0(gpu):
     import torch
     ode = gpu.Burgers(d_x=128, normalization='-11')
