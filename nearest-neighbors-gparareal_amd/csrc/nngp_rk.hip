@@ -224,16 +224,18 @@ __global__ void __launch_bounds__(64) rk_lane_kernel(LaneArgs args, int n_slices
 }
 
 // ---------------------------------------------------------------------------------------------
-// Lane-group kernel: one slice = one group of G lanes (G = 16 for the broadcast-coupled fields,
-// 4 for Thomas labyrinth), lane c owns component c (d <= 3, lanes c >= d are padding).
+// Lane-group kernel: one slice = one group of G lanes, each component on its own lanes: G = 16
+// (components in DPP banks, below) for every ODE but Thomas labyrinth, G = 4 (lane c = component c,
+// lane 3 padding) for Thomas labyrinth's rotation.
 // The lane kernel above runs every component's stage sums, (de)normalisation, h*k and final update
 // in one lane; here each of those is one instruction per step-part for all components at once, and
-// only the RHS coupling crosses lanes: `v_mov_b64_dpp row_newbcast:c` (gfx950's 64-bit DPP, one
-// VALU op) for G = 16, or a quad_perm rotation (two 32-bit DPP ops) for G = 4.
+// only the RHS coupling crosses lanes: `v_mov_b64_dpp row_newbcast` (gfx950's 64-bit DPP, one VALU
+// op) for G = 16, or a quad_perm rotation (two 32-bit DPP ops) for G = 4.
 // At few slices the step is one wave's instruction issue (a wave with 1 active
 // lane costs the same as 64), so fewer instructions per step is the whole gain, measured on the
-// box (tools/lane_group_probe.py): Hopf RK4 119 -> 101 VALU, 0.250 -> 0.207 us/step; Lorenz
-// 0.29 -> 0.21; Thomas labyrinth one sin per lane instead of three, 1.45 -> 0.52 us/step.
+// box (tools/lane_group_probe.py): Hopf RK4 119 -> 97 VALU, 0.250 -> 0.201
+// us/step; Lorenz 0.29 -> 0.19; Thomas labyrinth one sin per lane instead of three, 1.45 -> 0.52;
+// double pendulum one sincos per bank instead of three, 1.82 -> 0.97.
 // Bitwise the lane kernel: each component is rounded by the same expression in the same order.
 // ---------------------------------------------------------------------------------------------
 template <int CTRL>
@@ -258,8 +260,8 @@ __device__ __forceinline__ double take(double old, double v) {
     return __builtin_amdgcn_update_dpp(old, v, 0x150 + L, 0xF, BANKS, false);
 }
 
-// f(x = own de-normalised component, c = its index, one = 1.0) -> own component of f.  G16 (bank layout above)
-// for the broadcast-coupled fields (Lorenz, Hopf, Rossler), G4 (lane c = component c) for Thomas
+// f(x = own de-normalised component, c = its index, one = 1.0) -> own component of f.  G16 (bank
+// layout above) for the broadcast-coupled fields, G4 (lane c = component c) for Thomas
 // labyrinth's rotation (quad_perm, two 32-bit DPP ops).
 template <int SYS> struct GroupSys;
 
