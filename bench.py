@@ -277,25 +277,22 @@ def burgers_published_schedule(torch, g, sample_pages=2):
             'us_per_step': per_page / 39999 * 1e6}
 
 
-def tomlab_published_schedule(torch, g, sample_steps=1_000_000):
-    """The published Thomas labyrinth N=256 scalability run (TomLab.py:83-101: Nf = Ng*ceil(1e9/Ng),
-    RK4, RK_thresh = Nf/N/109) pages every slice into 110 pages of the full per-slice count
-    (new_lib.py:57-69): 4.30e8 RK4 steps per slice per iteration.  Time
-    `sample_steps` of them for all 256 slices (LINSPACE grid, lane-group kernel) and scale to the
-    iteration; the reference's F time per iteration on 282 cores was 156 s.  Each
-    slice is one serial chain, so this is per-step latency: a CPU core's 0.30-0.37 us/step vs one
-    GPU lane group's, with all 256 slices on one GPU instead of 282 cores."""
-    ode = g.ThomasLabyrinth(normalization='-11')
-    solver = g.SolverRK(ode.get_vector_field(), Ng=10, Nf=sample_steps, F='RK4', G='RK1',
+def ode_published_schedule(torch, g, ode, n, tspan, tab, eff, ref_s, ref_cores, sample_steps):
+    """One ODE's published scalability schedule: time `sample_steps` of its `eff` effective fine
+    steps per slice per iteration for all n slices (LINSPACE grids as the legacy RK_last, lane-group
+    kernel) and scale to the iteration, next to the reference's F time per iteration on its
+    cluster.  Each slice is one serial chain, so this compares per-step latency: a
+    CPU core per slice there, one GPU lane group per slice here."""
+    d = len(ode.get_init_cond())
+    solver = g.SolverRK(ode.get_vector_field(), Ng=10, Nf=sample_steps, F=tab, G='RK1',
                         step_mode='linspace', thresh=float('inf'))
-    n = 256
-    t = np.linspace(0, 100, n + 1)
+    small = g.SolverRK(ode.get_vector_field(), Ng=10, Nf=1000, F=tab, G='RK1', step_mode='linspace',
+                       thresh=float('inf'))
+    t = np.linspace(tspan[0], tspan[1], n + 1)
     dev = lambda a: torch.tensor(a, dtype=torch.float64, device='cuda')
     rng = np.random.default_rng(0)
-    U = dev(rng.uniform(-0.5, 0.5, (n, 3)))
+    U = dev(rng.uniform(-0.5, 0.5, (n, d)))
     out = torch.empty_like(U)
-    small = g.SolverRK(ode.get_vector_field(), Ng=10, Nf=1000, F='RK4', G='RK1', step_mode='linspace',
-                       thresh=float('inf'))
     small.run_F_batch(dev(t[:-1]), dev(t[1:]), U, out=out)
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -304,11 +301,26 @@ def tomlab_published_schedule(torch, g, sample_steps=1_000_000):
     b.record()
     torch.cuda.synchronize()
     us = a.elapsed_time(b) * 1e3 / sample_steps
-    eff = 4.30e8
     it = us * 1e-6 * eff
-    return {'us_per_step': us, 'F_per_iteration_s': it, 'reference_F_per_iteration_s': 156.0,
-            'reference_cores': 282, 'speedup_vs_reference_F': 156.0 / it, 'steps_per_slice': eff,
-            'sample': f'{sample_steps} of 4.30e8 steps x 256 slices, RK4, linspace'}
+    return {'us_per_step': us, 'F_per_iteration_s': it, 'reference_F_per_iteration_s': ref_s,
+            'reference_cores': ref_cores, 'speedup_vs_reference_F': ref_s / it, 'steps_per_slice': eff,
+            'sample': f'{sample_steps} of {eff:.3g} steps x {n} slices, {tab}, linspace'}
+
+
+def tomlab_published_schedule(torch, g, sample_steps=1_000_000):
+    """Thomas labyrinth N=256 (TomLab.py:83-101: Nf = Ng*ceil(1e9/Ng), RK4, RK_thresh = Nf/N/109):
+    110 pages of the full per-slice count (new_lib.py:57-69) = 4.30e8 RK4 steps per
+    slice per iteration; the reference's F per iteration on 282 cores was 156 s, 0.30-0.37 us/step."""
+    return ode_published_schedule(torch, g, g.ThomasLabyrinth(normalization='-11'), 256, (0, 100), 'RK4',
+                                  4.30e8, 156.0, 282, sample_steps)
+
+
+def hopf_published_schedule(torch, g, sample_steps=500_000):
+    """Hopf N=128 (Hopf.py:60-69: Nf x 10^4, RK8, RK_thresh = Nf/N/25): 3.4e8 effective RK8 steps per
+    slice per iteration (272 s / 0.80 us); the reference's F per iteration on 141
+    cores was 272 s."""
+    return ode_published_schedule(torch, g, g.Hopf(normalization='-11'), 128, (-20, 500), 'RK8',
+                                  3.4e8, 272.0, 141, sample_steps)
 
 
 def fhn_pde_fine_sweeps(torch, g):
@@ -418,6 +430,7 @@ def main():
         log('gparareal lorenz K', res['gparareal_lorenz_n32']['K'], f"{res['gparareal_lorenz_n32']['wall_s']:.2f}s")
         res['burgers_n128_published_schedule'] = burgers_published_schedule(torch, g)
         res['tomlab_n256_published_schedule'] = tomlab_published_schedule(torch, g)
+        res['hopf_n128_published_schedule'] = hopf_published_schedule(torch, g)
         res['fhn_pde_n512_fine_sweep'] = fhn_pde_fine_sweeps(torch, g)
         res['cpu_baseline'] = cpu_baseline(args.steps_per_slice, args.slices_per_gpu)
         # north-star target (>= 10x the CPU path on Burgers N=128, identical K): time the first
