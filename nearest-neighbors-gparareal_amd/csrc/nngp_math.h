@@ -112,9 +112,10 @@ struct TrigC {
 
 __device__ __forceinline__ void nn_sincos(double x, double &sn, double &cs) {
     const bool fin = x - x == 0.0;                 // finite
-    const double xf = fin ? x : 0.0;
-    const double n = rint(xf * TrigC::INVPIO2);
-    double r = fma(-n, TrigC::PIO2_1, xf);
+    // (the oracle zeroes a non-finite x before the reduction; its result is replaced by x - x below
+    // on both sides, so the kernel reduces x itself)
+    const double n = rint(x * TrigC::INVPIO2);
+    double r = fma(-n, TrigC::PIO2_1, x);
     r = fma(-n, TrigC::PIO2_2, r);
     r = fma(-n, TrigC::PIO2_3, r);
     const double z = r * r;
@@ -125,11 +126,15 @@ __device__ __forceinline__ void nn_sincos(double x, double &sn, double &cs) {
     const double hz = 0.5 * z;
     const double w = 1.0 - hz;
     const double kc = w + (((1.0 - w) - hz) + z * pc);
-    const int q = ((int)(n - 4.0 * floor(n * 0.25))) & 3;
+    // quadrant n mod 4 from the bit pattern of n + 1.5*2^52 (for |n| < 2^51 its low mantissa bits
+    // are n in two's complement; beyond, the same correctly rounded add on both sides): two ops
+    // instead of n - 4*floor(n/4) and a conversion
+    const int q = (int)((uint32_t)__double_as_longlong(n + 6755399441055744.0) & 3u);
     double s_ = (q & 1) ? kc : ks;
     double c_ = (q & 1) ? ks : kc;
-    s_ = (q & 2) ? -s_ : s_;
-    c_ = ((q + 1) & 2) ? -c_ : c_;
+    // sign flips as sign-bit xors (a negation is exactly that, so this is the oracle's `-s_`)
+    s_ = __longlong_as_double(__double_as_longlong(s_) ^ ((long long)(q & 2) << 62));
+    c_ = __longlong_as_double(__double_as_longlong(c_) ^ ((long long)((q + 1) & 2) << 62));
     const double nanv = x - x;                     // NaN for inf / NaN arguments
     sn = fin ? s_ : nanv;
     cs = fin ? c_ : nanv;

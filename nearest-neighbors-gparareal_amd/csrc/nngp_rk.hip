@@ -234,8 +234,8 @@ __global__ void __launch_bounds__(64) rk_lane_kernel(LaneArgs args, int n_slices
 // At few slices the step is one wave's instruction issue (a wave with 1 active
 // lane costs the same as 64), so fewer instructions per step is the whole gain, measured on the
 // box (tools/lane_group_probe.py): Hopf RK4 119 -> 97 VALU, 0.250 -> 0.201
-// us/step; Lorenz 0.29 -> 0.19; Thomas labyrinth one sin per lane instead of three, 1.45 -> 0.52;
-// double pendulum one sincos per bank instead of three, 1.82 -> 0.97.
+// us/step; Lorenz 0.29 -> 0.19; Thomas labyrinth one sin per lane instead of three, 1.45 -> 0.47;
+// double pendulum one sincos per bank instead of three, 1.82 -> 0.91.
 // Bitwise the lane kernel: each component is rounded by the same expression in the same order.
 // ---------------------------------------------------------------------------------------------
 template <int CTRL>

@@ -434,7 +434,11 @@ void nn_sincos(double x, double *sn, double *cs) {
     const double hz = 0.5 * z;
     const double w = 1.0 - hz;
     const double kc = w + (((1.0 - w) - hz) + z * pc);
-    const int q = ((int)(n - 4.0 * floor(n * 0.25))) & 3;
+    /* quadrant from the bit pattern of n + 1.5*2^52 (= n mod 4 for |n| < 2^51), as the kernel */
+    const double nq = n + 6755399441055744.0;
+    uint64_t nb;
+    memcpy(&nb, &nq, sizeof nb);
+    const int q = (int)(nb & 3u);
     double s_ = (q & 1) ? kc : ks;
     double c_ = (q & 1) ? ks : kc;
     s_ = (q & 2) ? -s_ : s_;
