@@ -11,7 +11,7 @@ import bench  # noqa: E402
 import nngp_amd as g  # noqa: E402
 
 torch.cuda.set_device(0)
-for thr in ('64', '128', '192', '256', '384', '512', '832', '1024'):
+for thr in ('64', '128', '192', '256', '320', '384', '448', '512', '832', '1024'):
     os.environ['NNGP_RK_THREADS'] = thr
     try:
         r = bench.fhn_pde_fine_sweeps(torch, g)
