@@ -132,7 +132,8 @@ int nngp_knn(const double *X, int64_t rows, int d, const double *q, int m, int32
  *   xm, ym: DEVICE [m][d]; coord, jitter_idx: DEVICE int32 [n_fits]; theta0: DEVICE [n_fits][2];
  *   jitter_exp_host: HOST [n_jitter] exponents (e.g. -20..-12, models.py:186);
  *   theta_out: DEVICE [n_fits][2]; fval_out: DEVICE [n_fits]; nfev_out: DEVICE int32 or NULL.
- * Requires 1 <= m <= 32.                                                                   */
+ * Requires 1 <= m <= 64 (fits padded to 8/16/20/24/32/48/64 rows; m > 32 runs 3-4 kernel rows
+ * per lane, one wave per workgroup).                                                        */
 int nngp_nm_fit_batch(int m, int d, const double *xm, const double *ym, int n_fits,
                       const int32_t *coord, const int32_t *jitter_idx, int n_jitter,
                       const double *jitter_exp_host, const double *theta0, double fatol,
@@ -153,7 +154,7 @@ int nngp_gp_mean(int m, int d, const double *xm, const double *ym, const double 
  * per-coordinate first-argmin of fval (models.py:207-215) and the posterior mean.
  *   preds_out = mean;  if bias != NULL also out = preds + bias (parareal.py:382).
  *   fits_out: DEVICE [n_fits][4] = (theta_x, theta_y, fval, nfev) or NULL.
- *   jitter_exp_host: HOST [n_jitter]. All other arrays DEVICE.  Requires 1 <= m <= 32.   */
+ *   jitter_exp_host: HOST [n_jitter]. All other arrays DEVICE.  Requires 1 <= m <= 64.   */
 int nngp_predict(const double *X, const double *Y, int64_t rows, int d, const double *new_x,
                  int m, int n_jitter, const double *jitter_exp_host, int n_restarts,
                  const double *theta0, double fatol, double xatol, int maxfev,

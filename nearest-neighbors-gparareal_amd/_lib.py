@@ -108,3 +108,12 @@ def require_gpu():
         raise NNGPError('no HIP device visible: nnGParareal-amd has no CPU fallback')
     lib()
     return torch
+
+
+def as_device(a):
+    """fp64 C-contiguous device tensor of a host array or a (device) tensor, without a copy when
+    it already is one (the driver hands the models its device-resident training set)."""
+    import torch
+    if torch.is_tensor(a):
+        return a.to(device='cuda', dtype=torch.float64).contiguous()
+    return torch.tensor(np.ascontiguousarray(a, dtype=np.float64), device='cuda')

@@ -230,7 +230,7 @@ __device__ __forceinline__ void row_key_min(uint64_t &bk, int &bi) {
 // the m smallest in order: a wave's lane t < 4m ranks its pair against all 4m, and a valid pair
 // of rank < m lands at that position (ok[]/oi[], or as index + value into oi32/od when ok null).
 template <typename KI>
-__device__ __forceinline__ void rank_merge(const uint64_t (*k)[32], const int (*ki)[32], int m, int lane, KI *ok,
+__device__ __forceinline__ void rank_merge(const uint64_t (*k)[64], const int (*ki)[64], int m, int lane, KI *ok,
                                            int *oi, double *od = nullptr) {
     const int n = 4 * m;
     for (int t = lane; t < n; t += 64) {
@@ -304,10 +304,10 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
     // 1) each 16-lane row of the workgroup: its m best (key, index) pairs among its lanes' rows
     //    (row r of the training set belongs to thread r % 256), in ascending order, by m rounds of
     //    "smallest pair strictly after the previous pick" with a 4-level DPP row minimum
-    __shared__ uint64_t rk[16][32];
-    __shared__ int ri[16][32];
-    __shared__ uint64_t wk[4][32];
-    __shared__ int wi[4][32];
+    __shared__ uint64_t rk[16][64];   // m <= 64
+    __shared__ int ri[16][64];
+    __shared__ uint64_t wk[4][64];
+    __shared__ int wi[4][64];
     {
         const int grp = tid >> 4;
         // K > 0: the thread's K keys (rows tid + 256*j) stay in registers for all m rounds
@@ -475,17 +475,31 @@ __device__ __forceinline__ void static_for(F &&f) {
     }
 }
 
-// A fit of size m runs padded to MAXM (one of 8, 16, 24, 32): rows m..MAXM-1 are identity rows
-// of K with y = 0.  The padded factorisation is exact -- L = [[L_m, 0], [0, I]], z and alpha
-// pad with exact zeros, every real row's arithmetic is untouched -- so every loop has a
+// A fit of size m runs padded to MAXM (one of 8, 16, 20, 24, 32, 48, 64): rows m..MAXM-1 are
+// identity rows of K with y = 0.  The padded factorisation is exact -- L = [[L_m, 0], [0, I]], z
+// and alpha pad with exact zeros, every real row's arithmetic is untouched -- so every loop has a
 // compile-time trip count and no per-j branches.
+// MAXM <= 32 (one or two rows per lane): the triangle's exps are spread evenly over the 16 lanes
+// and redistributed through a full LDS image (stride S).  MAXM > 32 (m > 32: the adaptive
+// m = max(10, k+2) past k = 30, or an explicit nn, models.py:172-175): three or four rows per
+// lane, each lane builds its own rows' exps in registers (no redistribution), and the LDS image
+// is the PACKED lower triangle (row r at r(r+1)/2) that only the back solve reads -- a full image
+// would not fit four fits per workgroup in LDS at m = 64.
 template <int MAXM_> struct GP {
     static constexpr int MAXM = MAXM_;
-    static constexpr int RPL = MAXM > 16 ? 2 : 1;                      // rows per lane
+    static constexpr int RPL = (MAXM + 15) / 16;                        // rows per lane
+    static constexpr bool BIG = MAXM > 32;
     static constexpr int S = MAXM + 1;                                  // LDS row stride (pad)
-    static constexpr int IMG = 16 * RPL * S;                            // image doubles / fit
-    static constexpr int NQ = (MAXM * (MAXM + 1) / 2 + 15) / 16;       // triangle entries / lane
+    static constexpr int IMG = BIG ? 8 * RPL * (16 * RPL + 1)           // image doubles / fit
+                                   : 16 * RPL * S;
+    static constexpr int NQ = BIG ? 1 : (MAXM * (MAXM + 1) / 2 + 15) / 16;   // triangle entries / lane
 };
+// LDS offset of K/L entry (r, j), j <= r, in a fit's image
+template <int MAXM>
+__device__ __forceinline__ int img_at(int r, int j) {
+    if constexpr (GP<MAXM>::BIG) return r * (r + 1) / 2 + j;
+    else return r * GP<MAXM>::S + j;
+}
 
 // per-lane, theta-independent part of a fit: where its share of the triangle lives
 // (idxq[q] = diagonal << 30 | D2 index << 16 | K-image slot; D2 index < 2^10, slot < 2^16)
@@ -499,6 +513,7 @@ __device__ __forceinline__ void gp_lane_init(GPLane<MAXM> &P, int m, int l) {
     constexpr int S = GP<MAXM>::S;
     const int T = m * (m + 1) / 2;
     P.nq = 0;
+    if constexpr (GP<MAXM>::BIG) return;   // rows are built by their owners (gp_factor)
     int r = 0;
 #pragma unroll
     for (int q = 0; q < GP<MAXM>::NQ; q++) {
@@ -518,6 +533,11 @@ __device__ __forceinline__ void gp_lane_init(GPLane<MAXM> &P, int m, int l) {
 template <int MAXM>
 __device__ __forceinline__ void gp_image_init(double *Kimg, int m, int l) {
     constexpr int RPL = GP<MAXM>::RPL, S = GP<MAXM>::S;
+    if constexpr (GP<MAXM>::BIG) {   // packed triangle: every pad-row entry (i >= m, j < i) is 0
+        for (int t = l; t < GP<MAXM>::IMG; t += 16) Kimg[t] = 0.0;
+        wave_lds_sync();
+        return;
+    }
 #pragma unroll
     for (int s = 0; s < RPL; s++) {
         const int row = l + 16 * s;
@@ -536,26 +556,45 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
                                           double (&alpha)[GP<MAXM>::RPL],
                                           double (&diag)[GP<MAXM>::RPL]) {
     constexpr int RPL = GP<MAXM>::RPL, S = GP<MAXM>::S, NQ = GP<MAXM>::NQ;
-    // 1) this lane's share of the triangle -> LDS image K[r*S + j]
-    wave_lds_sync();
+    double a[RPL][MAXM];
+    if constexpr (!GP<MAXM>::BIG) {
+        // 1) this lane's share of the triangle -> LDS image K[r*S + j]
+        wave_lds_sync();
 #pragma unroll
-    for (int q = 0; q < NQ; q++) {
-        if (q < P.nq) {
-            const int ix = P.idxq[q];
-            double e = psy * nn_exp(c * sD2[(ix >> 16) & 0x3FF]);    // k_gauss, models.py:146-148
-            if (ix >> 30) e = e + jit;                                // + eye*10**jitter, :88
-            Kimg[ix & 0xFFFF] = e;
+        for (int q = 0; q < NQ; q++) {
+            if (q < P.nq) {
+                const int ix = P.idxq[q];
+                double e = psy * nn_exp(c * sD2[(ix >> 16) & 0x3FF]);    // k_gauss, models.py:146-148
+                if (ix >> 30) e = e + jit;                                // + eye*10**jitter, :88
+                Kimg[ix & 0xFFFF] = e;
+            }
+        }
+        wave_lds_sync();
+        // 2) own rows into registers (pad rows are the image's identity rows; the upper triangle
+        //    is never used)
+#pragma unroll
+        for (int s = 0; s < RPL; s++)
+#pragma unroll
+            for (int j = 0; j < MAXM; j++)
+                if (j < 16 * (s + 1)) a[s][j] = Kimg[(l + 16 * s) * S + j];
+    } else {
+        // 1+2) each lane builds its own rows (the same expressions, models.py:146-148, 88); pad
+        //      rows are identity rows, the upper triangle zeros (never used)
+#pragma unroll
+        for (int s = 0; s < RPL; s++) {
+            const int row = l + 16 * s;
+#pragma unroll
+            for (int j = 0; j < MAXM; j++) {
+                if (j >= 16 * (s + 1)) continue;
+                double e = (row >= m && j == row) ? 1.0 : 0.0;
+                if (row < m && j <= row) {
+                    e = psy * nn_exp(c * sD2[row * m + j]);
+                    if (j == row) e = e + jit;
+                }
+                a[s][j] = e;
+            }
         }
     }
-    wave_lds_sync();
-    // 2) own rows into registers (pad rows are the image's identity rows; the upper triangle
-    //    is never used)
-    double a[RPL][MAXM];
-#pragma unroll
-    for (int s = 0; s < RPL; s++)
-#pragma unroll
-        for (int j = 0; j < MAXM; j++)
-            if (j < 16 * (s + 1)) a[s][j] = Kimg[(l + 16 * s) * S + j];
     // 3) left-looking Cholesky, row j broadcast from lane j%16 of set j/16.  The pivot is
     //    broadcast, so every lane computes L_jj and RN(1/L_jj) identically; the row owner keeps
     //    them.  Updates of rows < j (upper triangle) are computed and ignored: fewer
@@ -615,10 +654,17 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
     wave_lds_sync();
 #pragma unroll
     for (int s = 0; s < RPL; s++) {
-        if (l + 16 * s < m) {   // real rows only: the pad rows of the image stay identity
+        const int row = l + 16 * s;
+        if (row < m) {   // real rows only: the pad rows of the image stay identity (zero)
 #pragma unroll
-            for (int j = 0; j < MAXM; j++)
-                if (j < 16 * (s + 1)) Kimg[(l + 16 * s) * S + j] = a[s][j];
+            for (int j = 0; j < MAXM; j++) {
+                if (j >= 16 * (s + 1)) continue;
+                if constexpr (GP<MAXM>::BIG) {
+                    if (j <= row) Kimg[img_at<MAXM>(row, j)] = a[s][j];
+                } else {
+                    Kimg[row * S + j] = a[s][j];
+                }
+            }
         }
     }
     wave_lds_sync();
@@ -634,16 +680,18 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
         alpha[SI] = (l == LI) ? ai : alpha[SI];
 #pragma unroll
         for (int s = 0; s < RPL; s++)
-            if (16 * s < i) acc2[s] = acc2[s] - Kimg[i * S + l + 16 * s] * ai;   // L[i][row]
+            if (16 * s < i) acc2[s] = acc2[s] - Kimg[img_at<MAXM>(i, l + 16 * s)] * ai;   // L[i][row]
     });
     return !fail;
 }
 
-// sum over the fit's rows r < m of v[r] (pairs (l, l+16) first -- oracle butterfly_sum)
+// sum over the fit's rows r < m of v[r]: each lane adds its rows l, l+16, l+32, ... left to right
+// first, then the row butterfly (oracle butterfly_sum)
 template <int RPL>
 __device__ __forceinline__ double gp_rows_sum(int m, int l, const double (&v)[RPL]) {
     double p = (l < m) ? v[0] : 0.0;
-    if constexpr (RPL == 2) p = p + ((l + 16 < m) ? v[1] : 0.0);
+#pragma unroll
+    for (int s = 1; s < RPL; s++) p = p + ((l + 16 * s < m) ? v[s] : 0.0);
     return row_sum(p);
 }
 
@@ -745,8 +793,11 @@ __device__ __forceinline__ double jit_lookup(const NMArgs &a, int j) {
     return v;
 }
 
-// register budget: MAXM <= 16 fits 256 VGPRs (<= 512 threads), MAXM <= 32 needs up to 512 (256)
-template <int MAXM> struct NMBound { static constexpr int T = (MAXM <= 16) ? 512 : 256; };
+// register budget: MAXM <= 16 fits 256 VGPRs (<= 512 threads), MAXM <= 32 needs up to 512 (256);
+// MAXM > 32 (3-4 rows per lane) runs one wave per workgroup (LDS: four fit images, all registers)
+template <int MAXM> struct NMBound { static constexpr int T = (MAXM <= 16) ? 512 : (MAXM <= 32 ? 256 : 64); };
+// threads of the wave-per-fit speculative kernel and of the mean kernel
+template <int MAXM> struct WGT { static constexpr int T = MAXM > 32 ? 64 : 256; };
 
 template <int MAXM, bool FUSED>
 __global__ void __launch_bounds__(NMBound<MAXM>::T) nm_fit_kernel(NMArgs a) {
@@ -943,7 +994,7 @@ __device__ __forceinline__ int nm_candidates(const NM &S, NMCand (&c)[4]) {
 }
 
 template <int MAXM>
-__global__ void __launch_bounds__(256) nm_spec_kernel(NMArgs a) {
+__global__ void __launch_bounds__(WGT<MAXM>::T) nm_spec_kernel(NMArgs a) {
     constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG;
     extern __shared__ __attribute__((aligned(16))) double sm[];
     if (a.skip && *a.skip) return;   // uniform: the whole grid exits (speculation hit)
@@ -1050,7 +1101,7 @@ __global__ void __launch_bounds__(256) nm_spec_kernel(NMArgs a) {
 // of the coordinate's a.nj*a.R fits in a.fits_out (the unfused nngp_predict path, used when a
 // coordinate's fits do not fit one workgroup).  Writes a.preds[c] and a.out[c] = mean (+ bias).
 template <int MAXM>
-__global__ void __launch_bounds__(256) gp_mean_kernel(NMArgs a) {
+__global__ void __launch_bounds__(WGT<MAXM>::T) gp_mean_kernel(NMArgs a) {
     constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG;
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int m = a.m, d = a.d;
@@ -1114,9 +1165,37 @@ static int fill_jitters(NMArgs &a, int n_jitter, const double *jexp) {
     return NNGP_OK;
 }
 
-// padded fit size: the kernel instantiations (8, 16, 24, 32)
-static int maxm_for(int m) { return m <= 8 ? 8 : (m <= 16 ? 16 : (m <= 24 ? 24 : 32)); }
-static size_t k_image_doubles(int maxm) { return (size_t)16 * (maxm > 16 ? 2 : 1) * (maxm + 1); }
+// padded fit size: the kernel instantiations (8, 16, 20, 24, 32, 48, 64)
+static constexpr int MAX_M = 64;
+static int maxm_for(int m) {
+    return m <= 8 ? 8 : (m <= 16 ? 16 : (m <= 20 ? 20 : (m <= 24 ? 24 : (m <= 32 ? 32 : (m <= 48 ? 48 : 64)))));
+}
+static size_t k_image_doubles(int maxm) {
+    switch (maxm) {
+    case 8: return GP<8>::IMG;
+    case 16: return GP<16>::IMG;
+    case 20: return GP<20>::IMG;
+    case 24: return GP<24>::IMG;
+    case 32: return GP<32>::IMG;
+    case 48: return GP<48>::IMG;
+    default: return GP<64>::IMG;
+    }
+}
+static int wg_threads(int maxm) { return maxm > 32 ? 64 : 256; }
+
+// f<MAXM>() for the padded size of m
+template <typename F>
+static int with_maxm(int m, F &&f) {
+    switch (maxm_for(m)) {
+    case 8: return f(std::integral_constant<int, 8>{});
+    case 16: return f(std::integral_constant<int, 16>{});
+    case 20: return f(std::integral_constant<int, 20>{});
+    case 24: return f(std::integral_constant<int, 24>{});
+    case 32: return f(std::integral_constant<int, 32>{});
+    case 48: return f(std::integral_constant<int, 48>{});
+    default: return f(std::integral_constant<int, 64>{});
+    }
+}
 
 template <int MAXM>
 static int launch_nm(NMArgs &a, bool fused, int nblocks, int threads, size_t lds, hipStream_t st, int nq) {
@@ -1130,33 +1209,28 @@ static int launch_nm(NMArgs &a, bool fused, int nblocks, int threads, size_t lds
 
 static int run_mean(NMArgs &a, hipStream_t st) {
     const int maxm = maxm_for(a.m);
-    const int threads = 256, per = threads / 16;
+    const int threads = wg_threads(maxm), per = threads / 16;
     const size_t lds = sizeof(double) * ((size_t)a.m * a.m + a.m + (size_t)per * k_image_doubles(maxm));
     const dim3 grid((a.d + per - 1) / per);
-    switch (maxm) {
-    case 8: hipLaunchKernelGGL(gp_mean_kernel<8>, grid, dim3(threads), lds, st, a); break;
-    case 16: hipLaunchKernelGGL(gp_mean_kernel<16>, grid, dim3(threads), lds, st, a); break;
-    case 24: hipLaunchKernelGGL(gp_mean_kernel<24>, grid, dim3(threads), lds, st, a); break;
-    default: hipLaunchKernelGGL(gp_mean_kernel<32>, grid, dim3(threads), lds, st, a); break;
-    }
-    NNGP_LAUNCH_CHECK();
-    return NNGP_OK;
+    return with_maxm(a.m, [&](auto mc) {
+        hipLaunchKernelGGL(gp_mean_kernel<decltype(mc)::value>, grid, dim3(threads), lds, st, a);
+        NNGP_LAUNCH_CHECK();
+        return NNGP_OK;
+    });
 }
 
-// speculative kernel: one wave per fit, 4 fits per 256-thread workgroup
+// speculative kernel: one wave per fit, 4 fits per 256-thread workgroup (1 per 64-thread
+// workgroup for m > 32)
 static int run_nm_spec(NMArgs &a, hipStream_t st, int nq = 1) {
     const int maxm = maxm_for(a.m);
-    const int threads = 256;
+    const int threads = wg_threads(maxm);
     const size_t lds = sizeof(double) * ((size_t)a.m * a.m + (size_t)(threads / 16) * k_image_doubles(maxm));
     const dim3 grid((a.n_fits + threads / 64 - 1) / (threads / 64), nq);
-    switch (maxm) {
-    case 8: hipLaunchKernelGGL(nm_spec_kernel<8>, grid, dim3(threads), lds, st, a); break;
-    case 16: hipLaunchKernelGGL(nm_spec_kernel<16>, grid, dim3(threads), lds, st, a); break;
-    case 24: hipLaunchKernelGGL(nm_spec_kernel<24>, grid, dim3(threads), lds, st, a); break;
-    default: hipLaunchKernelGGL(nm_spec_kernel<32>, grid, dim3(threads), lds, st, a); break;
-    }
-    NNGP_LAUNCH_CHECK();
-    return NNGP_OK;
+    return with_maxm(a.m, [&](auto mc) {
+        hipLaunchKernelGGL(nm_spec_kernel<decltype(mc)::value>, grid, dim3(threads), lds, st, a);
+        NNGP_LAUNCH_CHECK();
+        return NNGP_OK;
+    });
 }
 
 // Speculative (a wave per fit) while the fits fit ~2 waves per SIMD (MAXM <= 16) or ~1 (MAXM 24/32,
@@ -1175,7 +1249,8 @@ static bool use_spec(int n_fits, int m) {
     static int ncu = 0;
     if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) ncu = 256;
     if (ncu <= 0) ncu = 256;
-    return n_fits <= (maxm_for(m) <= 16 ? 8 : 4) * ncu;
+    const int mm = maxm_for(m);   // m > 32: one fit per 64-thread workgroup, ~1 workgroup per CU (LDS)
+    return n_fits <= (mm <= 16 ? 8 : (mm <= 32 ? 4 : 1)) * ncu;
 }
 
 // fits per 16-lane group in the unfused kernel's work-queue mode (NNGP_NM_REFILL; 0/1 = off)
@@ -1192,7 +1267,7 @@ static int nm_fits_per_row() {
 static int run_nm(NMArgs &a, bool fused, hipStream_t st, int nq = 1) {
     const int maxm = maxm_for(a.m);
     const size_t kimg = k_image_doubles(maxm);
-    const int tmax = maxm <= 16 ? NMBound<16>::T : NMBound<32>::T;
+    const int tmax = maxm <= 16 ? NMBound<16>::T : (maxm <= 32 ? NMBound<32>::T : NMBound<64>::T);
     auto lds_of = [&](int threads) {
         const int galloc = threads / 16;
         return sizeof(double) * ((size_t)a.m * a.m + a.m + 4 * (size_t)galloc + (size_t)galloc * kimg);
@@ -1223,7 +1298,7 @@ static int run_nm(NMArgs &a, bool fused, hipStream_t st, int nq = 1) {
         a.cpw = 1;
         a.queue = nullptr;
     } else {
-        threads = 256;
+        threads = std::min(256, tmax);
         nblocks = (a.n_fits + threads / 16 - 1) / (threads / 16);
         a.cpw = 1;
         a.queue = nullptr;
@@ -1238,12 +1313,9 @@ static int run_nm(NMArgs &a, bool fused, hipStream_t st, int nq = 1) {
         }
     }
     const size_t lds = lds_of(threads);
-    switch (maxm) {
-    case 8: return launch_nm<8>(a, fused, nblocks, threads, lds, st, nq);
-    case 16: return launch_nm<16>(a, fused, nblocks, threads, lds, st, nq);
-    case 24: return launch_nm<24>(a, fused, nblocks, threads, lds, st, nq);
-    default: return launch_nm<32>(a, fused, nblocks, threads, lds, st, nq);
-    }
+    return with_maxm(a.m, [&](auto mc) {
+        return launch_nm<decltype(mc)::value>(a, fused, nblocks, threads, lds, st, nq);
+    });
 }
 
 // evaluation count at which the packed kernel parks a fit for the speculative kernel
@@ -1305,7 +1377,7 @@ extern "C" int nngp_nm_fit_batch(int m, int d, const double *xm, const double *y
                                  const double *jitter_exp_host, const double *theta0, double fatol,
                                  double xatol, int maxfev, double *theta_out, double *fval_out,
                                  int32_t *nfev_out, void *stream) {
-    NNGP_REQUIRE(m >= 1 && m <= 32, "need 1 <= m <= 32 (got %d)", m);
+    NNGP_REQUIRE(m >= 1 && m <= MAX_M, "need 1 <= m <= %d (got %d)", MAX_M, m);
     NNGP_REQUIRE(d >= 1 && n_fits >= 0, "bad d / n_fits");
     if (n_fits == 0) return NNGP_OK;
     NNGP_REQUIRE(xm && ym && coord && jitter_idx && theta0, "null array argument");
@@ -1332,7 +1404,7 @@ extern "C" int nngp_nm_fit_batch(int m, int d, const double *xm, const double *y
 extern "C" int nngp_gp_mean(int m, int d, const double *xm, const double *ym, const double *new_x,
                             const double *theta, const int32_t *jitter_idx, int n_jitter,
                             const double *jitter_exp_host, double *out, void *stream) {
-    NNGP_REQUIRE(m >= 1 && m <= 32, "need 1 <= m <= 32 (got %d)", m);
+    NNGP_REQUIRE(m >= 1 && m <= MAX_M, "need 1 <= m <= %d (got %d)", MAX_M, m);
     NNGP_REQUIRE(xm && ym && new_x && theta && jitter_idx && out, "null array argument");
     hipStream_t st = (hipStream_t)stream;
     NMArgs jt{};
@@ -1368,7 +1440,7 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
     NNGP_REQUIRE(X && Y && new_x && theta0 && preds_out, "null array argument");
     if (c1 < 0) c1 = d;
     NNGP_REQUIRE(0 <= c0 && c0 < c1 && c1 <= d, "bad coordinate range [%d, %d) of d=%d", c0, c1, d);
-    NNGP_REQUIRE(m >= 1 && m <= 32, "need 1 <= m <= 32 (got %d)", m);
+    NNGP_REQUIRE(m >= 1 && m <= MAX_M, "need 1 <= m <= %d (got %d)", MAX_M, m);
     NNGP_REQUIRE(m <= rows, "m=%d exceeds training rows=%lld", m, (long long)rows);
     NNGP_REQUIRE(d >= 1 && n_restarts >= 1 && maxfev >= 1, "bad d / n_restarts / maxfev");
     const bool spec = spec_idx && spec_fits && hit_flag;
@@ -1440,7 +1512,7 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
                int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
                double fatol, double xatol, int maxfev, int32_t *idx_out, double *fits_out, bool latency,
                hipStream_t st) {
-    NNGP_REQUIRE(nq >= 1 && m >= 1 && m <= 32 && m <= rows, "bad speculative batch shape");
+    NNGP_REQUIRE(nq >= 1 && m >= 1 && m <= MAX_M && m <= rows, "bad speculative batch shape");
     NMArgs a{};
     int rc = fill_jitters(a, n_jitter, jitter_exp_host);
     if (rc) return rc;

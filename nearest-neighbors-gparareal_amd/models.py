@@ -29,6 +29,7 @@ import numpy as np
 from . import _lib
 
 JITTERS = np.arange(-20, -11, dtype=float)   # models.py:186
+MAX_NEIGHBOURS = 64   # the HIP fits' largest padded kernel size (include/nngp.h)
 
 
 class ModelAbstr():
@@ -131,6 +132,8 @@ class NNGP_p(ModelAbstr):
         self.train_count = 0
         self.k = 0
         self._dev_xy = None
+        if self.nn != 'adaptive' and not 1 <= int(self.nn) <= MAX_NEIGHBOURS:
+            raise ValueError(f'nn={self.nn}: the GPU nnGP correction supports 1..{MAX_NEIGHBOURS} neighbours')
 
     # ------------------------------------------------------------------------------ helpers
     @property
@@ -138,7 +141,11 @@ class NNGP_p(ModelAbstr):
         return self.n * len(JITTERS) * self.n_restarts
 
     def n_neighbours(self):
-        return max(10, self.k + 2) if self.nn == 'adaptive' else int(self.nn)   # models.py:172-175
+        m = max(10, self.k + 2) if self.nn == 'adaptive' else int(self.nn)   # models.py:172-175
+        if m > MAX_NEIGHBOURS:   # adaptive m = k+2 passes the bound at iteration k = 63
+            raise ValueError(f"nn='adaptive' asks for m={m} neighbours at iteration {self.k}; the GPU nnGP "
+                             f'correction supports up to {MAX_NEIGHBOURS}')
+        return m
 
     def draw_thetas(self, n_predictions):
         """Initial thetas for `n_predictions` consecutive predictions (models.py:192)."""
@@ -179,9 +186,8 @@ class NNGP_p(ModelAbstr):
     def predict(self, new_x, prev_F=None, prev_G=None, *args, **kwargs):
         """models.py:171-183 (host arrays in/out; kNN + fits + argmin + mean on the GPU)."""
         torch = _lib.require_gpu()
-        if self._dev_xy is None:
-            self._dev_xy = (torch.tensor(np.ascontiguousarray(self.x, dtype=np.float64), device='cuda'),
-                            torch.tensor(np.ascontiguousarray(self.y, dtype=np.float64), device='cuda'))
+        if self._dev_xy is None:   # fit() may have been given host arrays or device tensors
+            self._dev_xy = (_lib.as_device(self.x), _lib.as_device(self.y))
         X, Y = self._dev_xy
         q = torch.tensor(np.asarray(new_x, dtype=np.float64).reshape(-1), device='cuda')
         th0 = torch.tensor(self.draw_thetas(1), device='cuda')
@@ -418,8 +424,7 @@ class GPjax_p(ModelAbstr):
         """models.py:420-425."""
         torch = _lib.require_gpu()
         self.k = k
-        X = torch.tensor(np.ascontiguousarray(x, dtype=np.float64), device='cuda')
-        Y = torch.tensor(np.ascontiguousarray(y, dtype=np.float64), device='cuda')
+        X, Y = _lib.as_device(x), _lib.as_device(y)
         new_hyp = self._train(X, Y, self.thetas)
         if k + 1 < self.hyp.shape[-1]:
             self.hyp[..., k + 1] = new_hyp

@@ -11,8 +11,9 @@ Per iteration k (parareal.py:301-439):
      model prediction (nngp_predict, or the classic F-G update), u[i+1] = preds + uG[i+1] -- all
      queued on one HIP stream without host synchronisation; the sweep is replicated on every rank
      (same inputs, same RNG draws), so ranks stay bit-identical without a broadcast.
-  4. one device->host copy of the new column, then the error / convergence scan (:396-416) on
-     the host exactly as the reference does.
+  4. the slice errors ||u^{k+1} - u^k||_inf on the device, then ONE device->host copy per
+     iteration (new iterate, coarse column, new D rows, errors) for the result dict and the
+     convergence scan (:396-416), which advances I on the host exactly as the reference does.
 The returned dict has the reference's keys ('t', 'u', 'err', 'x', 'D', 'k', 'data_x', 'data_D',
 'timings', 'debug_dict', 'converged', 'conv_int').
 """
@@ -383,7 +384,7 @@ class Parareal():
                 ctypes.byref(cs), _lib.TABLEAU[solver.G], solver.step_mode, solver.Ng, t_dev.data_ptr(), I, N,
                 U1.data_ptr(), UG1.data_ptr(), UF.data_ptr(), UG.data_ptr(), _lib.MODEL_NNGP, X.data_ptr(),
                 Y.data_ptr(), int(rows), m, len(jit), jp, model.n_restarts, th0.data_ptr(), float(model.fatol),
-                float(model.xatol), model.maxfev, self._preds_scratch.data_ptr(), self.speculate,
+                float(model.xatol), model.maxfev, self._preds_scratch.data_ptr(), self._run_speculate,
                 ctypes.byref(hits), ctypes.byref(g_ms), stream))
             model.train_count += model.n_fits * (N - I)
             self.spec_hits.append(int(hits.value))
@@ -402,16 +403,18 @@ class Parareal():
         return g_ms.value / 1e3
 
     def _shard_corrections(self, model):
-        """Shard each prediction's fits by coordinate over the process group: run(...,
-        shard_corrections=True/False), default when more than one rank and d*9*R >= 2048."""
+        """Shard each prediction's fits by coordinate over the process group: Parareal(...,
+        shard_corrections=True/False) or run(..., shard_corrections=...) for one run; default when
+        more than one rank and d*9*R >= 2048."""
         import torch
         dist = torch.distributed
         if self.process_group is None and not (dist.is_available() and dist.is_initialized()):
             return False
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(self.process_group) == 1:
             return False
-        if self.shard_corrections is not None:
-            return bool(self.shard_corrections)
+        shard = getattr(self, '_run_shard', self.shard_corrections)
+        if shard is not None:
+            return bool(shard)
         return model.n_fits >= 2048
 
     def _correction_sweep_sharded(self, torch, model, t_dev, I, N, U1, UG1, X, Y, rows, th0, stream):
@@ -516,6 +519,9 @@ class Parareal():
             raise NotImplementedError('debug mode runs on one rank')
         one_step_error, all_pred_err = [], []   # debug (parareal.py:258-262)
         self.spec_hits = []
+        # run(..., speculate=, shard_corrections=) override the constructor's settings for this run
+        self._run_speculate = int(kwargs.get('speculate', self.speculate))
+        self._run_shard = kwargs.get('shard_corrections', self.shard_corrections)
         tspan, N, epsilon, n = self.tspan, self.N, self.epsilon, self.n
         solver = self.solver
         verbose = kwargs.get('verbose', self.verbose)
@@ -568,6 +574,8 @@ class Parareal():
             Uk.copy_(torch.tensor(u[:, :, kc + 1], **f64))
             UGk.copy_(torch.tensor(_resume['uG_cur'], **f64))
             k_start = kc + 1
+            if I == N:   # parareal.py:294-295
+                raise Exception('System has already converged')
 
         cap = max(4 * N, 64, 2 * x.shape[0])
         Xd = torch.empty((cap, n), **f64)
@@ -577,17 +585,21 @@ class Parareal():
             Xd[:rows] = torch.tensor(x, **f64)
             Dd[:rows] = torch.tensor(D, **f64)
         k = k_start
+        th_pin = None   # pinned host staging of the initial-theta draws (async upload)
         for k in range(k_start, N):
             if verbose == 'v':
                 print(f'{self.ode_name} {model.name} iteration number (out of {N}): {k + 1} ')
             e0 = ev.start()
             self._fine_sweep(torch, t_dev, Uk, UF, I, N, n)
             ev.stop(e0, 'F')
+            n_F = N - I                       # slices of this iteration's fine sweep
             Uk1 = Uk.clone()
             UGk1 = UGk.clone()
             Uk1[I + 1] = UF[I + 1]            # u[I+1,:,k+1:] = uF[I+1,:,k]   (:331-333)
             I = I + 1
-            # training data (:336-339): x += u[I-1:N,:,k]; D += uF[I:N+1,:,k] - uG[I:N+1,:,k]
+            # training data (:336-339): x += u[I-1:N,:,k]; D += uF[I:N+1,:,k] - uG[I:N+1,:,k].
+            # Appended on the device; the host copy of the new D rows travels with the iteration's
+            # single device->host copy below (no host round trip between F and the sweep).
             new = N + 1 - I
             if rows + new > Xd.shape[0]:
                 grow = max(2 * Xd.shape[0], rows + new)
@@ -597,36 +609,51 @@ class Parareal():
             _lib.check(lib.nngp_parareal_update(new * n, UF[I:N + 1].data_ptr(), UGk[I:N + 1].data_ptr(),
                                                 None, Dd[rows:rows + new].data_ptr(), stream))
             rows += new
-            d_new = Dd[rows - new:rows].cpu().numpy()
             x = np.vstack([x, u[I - 1:N, :, k]])
-            D = np.vstack([D, d_new])
             if not light:
                 data_x[I - 1:N, :, k] = u[I - 1:N, :, k]
-                data_D[I - 1:N, :, k] = d_new
-            fe = ev.collect()
-            F_time += fe.get('F', 0.0)
-            F_time_serial += fe.get('F', 0.0)   # every slice runs for the whole launch
+
+            def take_D(d_new):
+                nonlocal D
+                D = np.vstack([D, d_new])
+                if not light:
+                    data_D[I - 1:N, :, k] = d_new
 
             if I == N:                          # early stop (:343-348)
                 if verbose == 'v':
                     print('WARNING: early stopping')
+                take_D(Dd[rows - new:rows].cpu().numpy())
                 u[:, :, k + 1] = Uk1.cpu().numpy()
                 err[:, k] = np.linalg.norm(u[:, :, k + 1] - u[:, :, k], np.inf, 1)
                 last = k if light else k + 1   # PararealLight returns u_curr here
                 err[-1, k] = np.nextafter(epsilon, 0)
+                fe = ev.collect()
+                F_time += fe.get('F', 0.0)
+                F_time_serial += fe.get('F', 0.0)
                 break
 
             lag_k = kwargs.get('lag_k')
+            d_pending = True
             if lag_k is None:
-                model.fit_timed(x, D, k=k, data_x=data_x, data_y=data_D)
+                # the models train on the device-resident set (fit stores it; no host copy)
+                model.fit_timed(Xd[:rows], Dd[:rows], k=k, data_x=data_x, data_y=data_D)
                 Xs, Ds, rows_s = Xd, Dd, rows
             else:   # legacy: train on the last lag_k iterations only (new_lib.py:980-987)
+                take_D(Dd[rows - new:rows].cpu().numpy())
+                d_pending = False
                 tr_x = np.moveaxis(data_x[I:, :, max(k + 1 - lag_k, 0):k + 1], 1, -1).reshape(-1, n)
                 tr_y = np.moveaxis(data_D[I:, :, max(k + 1 - lag_k, 0):k + 1], 1, -1).reshape(-1, n)
                 model.fit_timed(tr_x, tr_y, k=k)
                 Xs, Ds, rows_s = torch.tensor(tr_x, **f64), torch.tensor(tr_y, **f64), tr_x.shape[0]
             if is_nngp:
-                th0 = torch.tensor(model.draw_thetas(N - I), **f64)
+                draws = torch.from_numpy(model.draw_thetas(N - I))
+                if th_pin is None or th_pin.numel() < draws.numel():
+                    th_pin = torch.empty(max(draws.numel(), 2 * N * model.n_fits), dtype=torch.float64,
+                                         pin_memory=True)
+                # the previous iteration's upload finished before its host copy below returned
+                th_pin[:draws.numel()].copy_(draws.view(-1))
+                th0 = torch.empty(draws.shape, **f64)
+                th0.view(-1).copy_(th_pin[:draws.numel()], non_blocking=True)
             e_loop = ev.start()
             if debug:
                 g_s, pred_err = self._correction_sweep_debug(torch, model, t_dev, I, N, Uk1, UGk1, UF, UGk, Xs, Ds,
@@ -638,15 +665,32 @@ class Parareal():
                 g_s = self._correction_sweep(torch, model, t_dev, I, N, Uk1, UGk1, UF, UGk, Xs, Ds, rows_s,
                                              th0 if is_nngp else None, stream)
             ev.stop(e_loop, 'loop')
-            u[:, :, k + 1] = Uk1.cpu().numpy()
+            # ONE device->host copy per iteration: the new iterate (the reference's u[:, :, k+1]),
+            # the new coarse column (NaN guard, checkpoint), the new D rows and the slice errors
+            # ||u^{k+1}_p - u^k_p||_inf (parareal.py:402-403; torch.amax propagates NaN as np.max).
+            errk = torch.amax(torch.abs(Uk1 - Uk), dim=1)
+            parts = [Uk1.reshape(-1), UGk1.reshape(-1), errk]
+            if d_pending:
+                parts.append(Dd[rows - new:rows].reshape(-1))
+            host = torch.cat(parts).cpu().numpy()
+            sz = (N + 1) * n
+            u[:, :, k + 1] = host[:sz].reshape(N + 1, n)
             last = k + 1
-            ug = UGk1.cpu().numpy()
+            ug = host[sz:2 * sz].reshape(N + 1, n)
+            if d_pending:
+                take_D(host[2 * sz + N + 1:].reshape(new, n))
             te = ev.collect()
+            F_time += te.get('F', 0.0)
+            # F_time_serial_avg (parareal.py:314): the per-slice fine time averaged over the
+            # iteration's slices.  Every slice of the batched launch runs from its start to its end
+            # (a lone slice takes as long: the chain of steps is the cost), so each slice's time is
+            # the launch's and so is their mean.
+            F_time_serial += te.get('F', 0.0) if n_F > 0 else 0.0
             G_time += g_s
             model.add_pred_time(max(te.get('loop', 0.0) - g_s, 0.0))
             if np.any(np.isnan(ug)):
                 raise Exception('NaN values in initial coarse solve - increase Ng!')
-            err[:, k] = np.linalg.norm(u[:, :, k + 1] - u[:, :, k], np.inf, 1)   # (:402-403)
+            err[:, k] = host[2 * sz:2 * sz + N + 1]                                # (:402-403)
             err[I, k] = 0
             if debug:   # (:405-406)
                 one_step_error.append([err[I + 1, k], pred_err.max()])
@@ -667,7 +711,9 @@ class Parareal():
                         'data_D': data_D[..., :k + 1], 'G_time': G_time, 'F_time': F_time,
                         'F_time_serial': F_time_serial, 'epsilon': epsilon, 'N': N,
                         'ode_name': self.ode_name}
-                self.store(name=f'{name_base}_{k}', path=kwargs.get('int_dir', ''), mdl=model, objs=objs)
+                # <int_dir>/<name_base>/<name_base>_<k>.npz, the reference's layout (parareal.py:422-431)
+                self.store(name=f'{name_base}_{k}', path=os.path.join(kwargs.get('int_dir', ''), name_base),
+                           mdl=model, objs=objs)
             if I == N:
                 break
             if (early_stop is not None) and k == (early_stop - 1):

@@ -28,8 +28,9 @@
  *   - kNN distance: sequential (scipy cdist sqeuclidean, transform_reduce_2d_)
  *   - Cholesky: left-looking, successive subtraction, scale by reciprocal (OpenBLAS potf2)
  *   - triangular solves: successive subtraction (OpenBLAS trsv column sweeps)
- *   - y^T alpha, sum(log diag L), K*^T alpha: balanced binary tree over G lanes (G = 16 for
- *     m <= 16, 32 for m <= 32), = the GPU's xor-butterfly reduction
+ *   - y^T alpha, sum(log diag L), K*^T alpha: per lane l the rows l, l+16, l+32, l+48 summed
+ *     left to right, then a balanced binary tree over the 16 lanes, = the GPU's xor-butterfly
+ *     reduction
  *   - x**3 = x*(x*x) (jax integer_pow), x**2 = x*x
  * Build: oracle/Makefile (gcc -O2 -fopenmp -ffp-contract=off).
  */
@@ -493,14 +494,15 @@ double orc_sqdist_pairwise(const double *a, const double *b, int d, double *scra
     return pairwise_sum(scratch, d);
 }
 
-/* Cross-lane sum of the GPU's 16-lane group (one DPP row): lane l holds rows l and, for
- * m > 16, l+16, which it adds first; then xor-butterfly levels 1, 2, 4, 8 -- lane 0 pairs
- * (0,1),(2,3),... first, then (0,2),... -- a balanced tree.  Rows >= n contribute 0.0.       */
+/* Cross-lane sum of the GPU's 16-lane group (one DPP row): lane l holds rows l, l+16, l+32,
+ * l+48 (as many as ceil(n/16)), which it adds first, left to right; then xor-butterfly levels
+ * 1, 2, 4, 8 -- lane 0 pairs (0,1),(2,3),... first, then (0,2),... -- a balanced tree.  Rows >= n
+ * contribute 0.0.                                                                            */
 static double butterfly_sum(const double *v, int n) {
     double buf[16];
     for (int i = 0; i < 16; i++) {
         buf[i] = i < n ? v[i] : 0.0;
-        if (n > 16) buf[i] = buf[i] + (i + 16 < n ? v[i + 16] : 0.0);
+        for (int s = 1; 16 * s < n; s++) buf[i] = buf[i] + (i + 16 * s < n ? v[i + 16 * s] : 0.0);
     }
     for (int s = 1; s < 16; s <<= 1)
         for (int i = 0; i < 16; i += 2 * s) buf[i] = buf[i] + buf[i + s];
@@ -778,7 +780,7 @@ void orc_knn(const double *X, int64_t rows, int d, const double *q, int m, int32
 int orc_predict(const double *X, const double *Y, int64_t rows, int d, const double *q, int m,
                 int nj, const double *jit_exp, int R, const double *theta0, double fatol,
                 double xatol, int maxfev, double *preds, double *fits_out, int nthreads) {
-    if (m < 1 || m > 32 || m > rows) return -1;
+    if (m < 1 || m > 64 || m > rows) return -1;   /* the GPU path's bound (m <= 64) */
     int32_t *idx = (int32_t *)malloc(sizeof(int32_t) * m);
     double *xm = (double *)malloc(sizeof(double) * m * d);
     double *ymT = (double *)malloc(sizeof(double) * m * d); /* [d][m] */

@@ -41,9 +41,9 @@ def test_argument_errors_are_reported_without_a_gpu():
     assert b'steps' in L.nngp_last_error()
     assert L.nngp_predict(None, None, 10, 3, None, 5, 9, None, 1, None, 0.1, 0.1, 400, None, None, None,
                           None, None) == -1
-    assert L.nngp_nm_fit_batch(40, 3, None, None, 1, None, None, 9, None, None, 0.1, 0.1, 400, None, None,
+    assert L.nngp_nm_fit_batch(65, 3, None, None, 1, None, None, 9, None, None, 0.1, 0.1, 400, None, None,
                                None, None) == -1
-    assert b'm <= 32' in L.nngp_last_error()
+    assert b"m <= 64" in L.nngp_last_error()
     assert L.nngp_rk_batch(ctypes.byref(cs), 4, 0, 0, None, None, 10, None, None, None) == 0   # empty batch
 
 

@@ -169,6 +169,6 @@ def test_gparareal_checkpoint_resume_is_bitwise(gpu, tmp_path):
     full = gpu.Parareal(ode, s, [0, 18], 32, epsilon=5e-7, verbose=None).run(
         model='gpjax', store_int=True, int_dir=str(tmp_path), int_name='gp', early_stop=6)
     p = gpu.Parareal(ode, s, [0, 18], 32, epsilon=5e-7, verbose=None)
-    res = p.load_int_dump(str(tmp_path / 'gp_2.npz'), early_stop=6)
+    res = p.load_int_dump(str(tmp_path / 'gp' / 'gp_2.npz'), early_stop=6)
     assert res['k'] == full['k'] and res['conv_int'] == full['conv_int']
     assert np.array_equal(np.nan_to_num(res['u'], nan=7.0), np.nan_to_num(full['u'], nan=7.0))

@@ -167,10 +167,10 @@ def test_parareal_update_kernel(gpu):
 
 
 # ---------------------------------------------------------------------------------- GP pieces
-@pytest.mark.parametrize('rows,d,m', [(640, 3, 10), (3000, 128, 15), (700, 200, 20), (33, 3, 33), (5000, 2, 12), (1100, 128, 15)])
+@pytest.mark.parametrize('rows,d,m', [(640, 3, 10), (3000, 128, 15), (700, 200, 20), (33, 3, 33), (5000, 2, 12),
+                                     (1100, 128, 15), (2000, 128, 64), (90, 5, 48)])
 def test_knn_vs_oracle(gpu, rows, d, m):
     import torch
-    m = min(m, 32)
     rng = np.random.default_rng(rows + d)
     X = rng.standard_normal((rows, d))
     X[5] = X[rows // 2]                          # exact duplicate -> tie broken by index
@@ -271,9 +271,11 @@ def test_predict_restarts_and_small_training_set(gpu):
 
 @pytest.mark.parametrize('park', ['0', '30', '100'])
 @pytest.mark.parametrize('m,d,R', [(5, 3, 1), (12, 4, 2), (16, 3, 2), (20, 6, 1), (20, 3, 2), (30, 2, 2),
-                                   (10, 300, 1), (18, 130, 2), (20, 80, 1)])
+                                   (10, 300, 1), (18, 130, 2), (20, 80, 1), (24, 3, 1),
+                                   (40, 3, 1), (48, 4, 2), (64, 3, 1), (56, 40, 1), (33, 140, 1)])
 def test_predict_every_padded_size_and_fallback_vs_oracle(gpu, m, d, R, park, monkeypatch):
-    """Fits run padded to 8/16/24/32 rows (identity pad, exact).  Up to 8 fits per CU each fit
+    """Fits run padded to 8/16/20/24/32/48/64 rows (identity pad, exact; m > 32 -- the adaptive
+    m = max(10, k+2) past iteration 30, models.py:172-175 -- with 3-4 kernel rows per lane).  Up to 8 fits per CU each fit
     gets a wave and evaluates reflect/expand/contract points speculatively; above that (d=300:
     2 700 fits) the packed kernel runs 4 fits per wave, fused with the arg-min and mean -- or,
     when a coordinate's fits exceed a workgroup (m=18, R=2 at d=130: 4 680 fits), as fits +
@@ -347,3 +349,30 @@ def test_fhn_pde_full_size_vs_oracle(gpu, nx, n_slices, norm):
     assert np.all(np.isfinite(out))
     for i in sorted({0, 1, n_slices // 2, n_slices - 1}):
         assert np.array_equal(out[i], so.rk(8, T[i], T[i + 1], 6, U0[i], O.STEP_FIXED)), i
+
+
+def test_predict_fhn_pde_d800_vs_oracle(gpu):
+    """BASELINE configs[4]'s correction shape: FHN-PDE d = 800, m = 20, R = 1 (FHN_PDE.py:175-176):
+    7 200 fits per prediction -- the packed fits kernel with the tail hand-off (fits still running
+    at 70 evaluations are parked and finished by the speculative kernel), then the arg-min + mean
+    kernel -- bitwise the oracle's fits and prediction."""
+    import torch
+    d, rows, m = 800, 1500, 20
+    rng = np.random.default_rng(800)
+    X = np.clip(np.cumsum(0.01 * rng.standard_normal((rows, d)), axis=0), -1, 1)
+    Y = 0.02 * np.sin(2 * X) + 1e-5 * rng.standard_normal(X.shape)
+    q = X[rows // 3] + 1e-3
+    mdl = gpu.NNGP_p(n=d, N=4, nn=m, n_restarts=1, seed=45)
+    th0 = mdl.draw_thetas(1)
+    assert mdl.n_fits == 7200
+    fits = torch.empty((mdl.n_fits, 4), dtype=torch.float64, device='cuda')
+    bias = rng.standard_normal(d)
+    out = torch.empty(d, dtype=torch.float64, device='cuda')
+    preds = mdl.predict_device(_t(torch, X), _t(torch, Y), rows, _t(torch, q), _t(torch, th0), fits_out=fits,
+                               out=out, bias=_t(torch, bias)).cpu().numpy()
+    ora, ofits = O.predict(X, Y, q, m, th0, return_fits=True)
+    f = fits.cpu().numpy()
+    assert np.array_equal(f, ofits)
+    assert np.array_equal(preds, ora)
+    assert np.array_equal(out.cpu().numpy(), ora + bias)
+    print('FHN-PDE d=800 nfev mean %.1f max %d' % (f[:, 3].mean(), f[:, 3].max()))

@@ -145,6 +145,17 @@ def test_speculative_sweep_is_bitwise_and_hits(gpu, case, window, monkeypatch):
     assert sum(hits) > 0 and a['timings']['spec_hits'] == [0] * len(hits)
 
 
+def test_run_kwargs_override_constructor_settings(gpu):
+    """run(..., speculate=...) applies to that run only (the constructor's value otherwise)."""
+    ode = gpu.Lorenz(normalization='-11')
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=6, Nf=450, F='RK4', G='RK4')
+    p = gpu.Parareal(ode, s, [0, 18], 32, epsilon=5e-7, verbose=None, speculate=1)
+    a = p.run(model='nngp', nn=10, seed=47, early_stop=3, speculate=0)
+    b = p.run(model='nngp', nn=10, seed=47, early_stop=3)
+    assert a['timings']['spec_hits'] == [0] * a['k'] and sum(b['timings']['spec_hits']) > 0
+    assert np.array_equal(np.nan_to_num(a['u'], nan=7.0), np.nan_to_num(b['u'], nan=7.0))
+
+
 @pytest.mark.parametrize('model', ['nngp', 'parareal', 'gpjax'])
 def test_debug_mode_reports_prediction_errors_without_changing_the_run(gpu, model):
     """run(debug=True) (parareal.py:258-262, 353-406, 441-463): the same iterates, plus per
@@ -182,3 +193,20 @@ def test_pararealight_returns_the_newest_iterate(gpu, model):
     assert np.array_equal(light['x'], full['x'][:light['x'].shape[0]])
     with pytest.raises(NotImplementedError):
         gpu.PararealLight(ode, s, [0, 18], 32, verbose=None).run(model=model, store_int=True, **kw)
+
+
+@pytest.mark.parametrize('F', ['RK4', 'RK8'])
+def test_hopf_n128_nngp_bitwise_equals_oracle_loop(gpu, F):
+    """BASELINE configs[1], Hopf N=128 on the configs.py schedule (configs.py:35-46: Ng/N = 16 RK1,
+    Nf/N = 1 360; F = RK4 as BASELINE names it, RK8 as configs.py has it) with Hopf.py's nnGP
+    settings (nn=15, n_restarts=2, fatol=xatol=0.1, seed 45; Hopf.py:83-84): every iterate, K and
+    the converged-interval sequence equal the oracle's loop bit for bit (speculative sweep on)."""
+    ode = gpu.Hopf(normalization='-11')
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=16, Nf=1360, F=F, G='RK1')
+    kw = dict(nn=15, n_restarts=2, fatol=0.1, xatol=0.1, seed=45)
+    r = gpu.Parareal(ode, s, [-20, 500], 128, epsilon=5e-7, verbose=None).run(model='nngp', **kw)
+    so = O.System('hopf', param=(500.0,))
+    o = O.parareal(so, [-20, 500], 128, 16, 1360, 'RK1', F, model='nngp', u0=so.fit([0.1, 0.1, -20]), **kw)
+    print('Hopf N=128', F, 'K', r['k'], 'conv_int', r['conv_int'], 'spec hits', r['timings']['spec_hits'])
+    assert r['converged'] and r['k'] == o['k'] and r['conv_int'] == o['conv_int']
+    assert np.array_equal(np.nan_to_num(r['u'], nan=7.0), np.nan_to_num(o['u'], nan=7.0))

@@ -155,3 +155,20 @@ def test_report_tables_layout():
     x = p.print_speedup(F_t=0.1, md=False, mdl_title='Lorenz').split('\n')
     assert x[0] == r'\caption*{Lorenz, $N=32$}' and x[3] == r'\hline\\'
     assert x[-3].endswith('& ' + f'{3.2 / (0.1 * 19 + 0.2):.2f}' + r'\\')
+
+
+def test_nngp_neighbour_bound_is_explicit():
+    """The GPU fits support m <= 64 neighbours: an explicit nn beyond that is refused at
+    construction, and nn='adaptive' (m = max(10, k+2), models.py:172-175) raises a clear error
+    once k+2 passes it, instead of failing inside a kernel launch."""
+    import nngp_amd
+    with pytest.raises(ValueError):
+        nngp_amd.NNGP_p(n=3, N=100, nn=65)
+    mdl = nngp_amd.NNGP_p(n=3, N=100, nn=64)
+    assert mdl.n_neighbours() == 64
+    ad = nngp_amd.NNGP_p(n=3, N=100)
+    ad.k = 62
+    assert ad.n_neighbours() == 64
+    ad.k = 63
+    with pytest.raises(ValueError, match='adaptive'):
+        ad.n_neighbours()
