@@ -147,7 +147,7 @@ def converge(torch, g, which):
     r = p.run(model='nngp', **kw)
     torch.cuda.synchronize()
     r['timings']['conv_int'] = list(r['conv_int'])
-    return time.perf_counter() - t0, r['k'], r['converged'], r['timings']
+    return time.perf_counter() - t0, r['k'], r['converged'], r['timings'], r
 
 
 def corrections_fhn_d200(torch, g, n_pred=20):
@@ -176,6 +176,75 @@ def corrections_fhn_d200(torch, g, n_pred=20):
             'ratio_vs_reference': n_pred / s / 1.54}
 
 
+def fhn_pde_converge(torch, g, dx=20, ng=50, nf=195325):
+    """BASELINE configs[4] end to end on one GPU: FHN-PDE d = 2*20^2 = 800, N = 512, nnGParareal
+    m = 20 (FHN_PDE.py:175), T = 1100 (configs.py:128-139's default branch), F = RK8 with
+    FHN_PDE.py's 1e8 schedule (Nf = ceil(1e8/12800)*12800 -> 195 325 steps per slice, unpaged).
+    G = RK4 with 50 steps per slice: the default branch's 25 diverge at d_x = 20 (h*lambda_min =
+    -3.96 for the stiffest diffusion mode, outside RK4's real stability interval [-2.79, 0]; the
+    reference's own NaN guard raises 'NaN values in initial coarse solve'), and its smoke F of 25
+    RK8 steps per slice diverges too."""
+    ode = g.FHN_PDE(d_x=dx)
+    solver = g.SolverRK(ode.get_vector_field(), Ng=ng, Nf=nf, F='RK8', G='RK4', thresh=float('inf'))
+    p = g.Parareal(ode, solver, [0, 1100], 512, epsilon=5e-7, verbose=None)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r = p.run(model='nngp', nn=20, seed=45)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    tm = r['timings']
+    return {'wall_s': wall, 'K': r['k'], 'converged': r['converged'], 'conv_int': list(r['conv_int']),
+            'F_time_s': tm['F_time'], 'G_time_s': tm['G_time'], 'mdl_time_s': tm['mdl_tot_t'],
+            'd': ode.d, 'N': 512, 'Ng_per_slice': ng, 'Nf_per_slice': nf, 'm': 20,
+            'spec_hits': tm.get('spec_hits', [])}
+
+
+def _maxm(m):
+    for M in (8, 16, 20, 24, 32, 48, 64):
+        if m <= M:
+            return M
+    return m
+
+
+def correction_roofline(torch, g, d, m, R=1, rows=3000, reps=3):
+    """Roofline of one nnGP correction (NNGP_p.predict = kNN + d*9*R Nelder-Mead fits + arg-min +
+    posterior mean, models.py:171-226): algorithmic flops = sum over fits of nfev x (m^3/3 + 2m^2
+    + 4m) -- the jittered Cholesky, both triangular solves and the -LML sums of one likelihood
+    evaluation, plus m(m+1)/2 exps counted separately -- over the correction's
+    device time (HIP events on the launch stream), against the FP64 VALU peak.  The kernels run
+    padded to the next instantiated size M; the executed flops at M are reported beside."""
+    rng = np.random.default_rng(d + m)
+    X = np.clip(np.cumsum(0.01 * rng.standard_normal((rows, d)), axis=0), -1, 1)
+    Y = 0.02 * np.sin(2 * X) + 1e-5 * rng.standard_normal((rows, d))
+    dev = lambda a: torch.tensor(a, dtype=torch.float64, device='cuda')
+    Xt, Yt = dev(X), dev(Y)
+    mdl = g.NNGP_p(n=d, N=4, nn=m, n_restarts=R, seed=45)
+    th0 = dev(mdl.draw_thetas(1))
+    q = Xt[rows // 3] + 1e-3
+    fits = torch.empty((mdl.n_fits, 4), dtype=torch.float64, device='cuda')
+    mdl.predict_device(Xt, Yt, rows, q, th0, fits_out=fits)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        mdl.predict_device(Xt, Yt, rows, q, th0, fits_out=fits)
+    b.record()
+    torch.cuda.synchronize()
+    sec = a.elapsed_time(b) / 1e3 / reps
+    nfev = fits[:, 3].cpu().numpy()
+    M = _maxm(m)
+    per = m ** 3 / 3 + 2 * m ** 2 + 4 * m
+    per_M = M ** 3 / 3 + 2 * M ** 2 + 4 * M
+    ev = float(nfev.sum())
+    tf = ev * per / sec / 1e12
+    return {'d': d, 'm': m, 'R': R, 'rows': rows, 'fits': mdl.n_fits, 'ms_per_correction': sec * 1e3,
+            'evaluations': ev, 'nfev_mean': float(nfev.mean()), 'nfev_max': int(nfev.max()),
+            'flops_per_evaluation': per, 'exps_per_evaluation': m * (m + 1) / 2, 'padded_to': M,
+            'achieved_tflops': tf, 'frac_fp64_peak': tf / FP64_PEAK_TFLOPS,
+            'executed_tflops_padded': ev * per_M / sec / 1e12,
+            'note': 'latency-bound: a correction waits for its slowest fit (nfev_max evaluations in sequence)'}
+
+
 def gparareal_lorenz(torch, g):
     """Full-data GParareal (model='gpjax') on BASELINE configs[0], Lorenz N=32.  The reference's
     own run of this config (tests/golden/gp_lorenz.npz, gen_golden.py part_gp) took 247 s with
@@ -193,11 +262,68 @@ def gparareal_lorenz(torch, g):
             'speedup_vs_reference_quoted': 247.0 / wall}
 
 
-def cpu_baseline(steps_per_slice_full, n_slices, target_s=10.0):
-    """Oracle C restatement (OpenMP over slices) on a bounded sample of the fine sweep."""
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import oracle as O
-    threads = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or len(os.sched_getaffinity(0))
+    return O
+
+
+def cpu_threads():
+    return int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or len(os.sched_getaffinity(0))
+
+
+def cpu_model():
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_single_core(budget_s=0.4):
+    """One host core's us per fine step of the CPU restatement (oracle/nngp_oracle.c, gcc -O3
+    -march=x86-64-v4), next to the reference's per-core figures (its XLA-CPU path,
+    one MPI worker core per slice).  PDE fields twice: the stencil port and the reference's dense
+    formulation (Dxx@u / (a L)@u1 as full matrices, systems.py:321-446 -- the same results, bit
+    for bit, at the reference's d^2 cost).  The BASELINE.md E sanity bar: within ~2x."""
+    O = _oracle()
+    x128 = np.linspace(-1, 1, 128)
+    rng = np.random.default_rng(0)
+    cases = [
+        ('hopf_rk8', lambda dn: O.System('hopf', param=(500.0,)), 8, np.array([0.1, 0.1, -0.9]), 0.80),
+        ('tomlab_rk4', lambda dn: O.System('tomlab'), 4, np.array([0.3, 0.1, -0.2]), 0.30),
+        ('burgers_d128_rk8', lambda dn: O.System('burgers', d=128, param=(0.01,), mn=0.0, mx=1.0, dense=dn), 8,
+         0.5 * (np.cos(4.5 * np.pi * x128) + 1) * 2 - 1, 46.6),
+        ('fhn_pde_d200_rk8', lambda dn: O.System('fhn_pde', nx=10, mn=-1, mx=1, dense=dn), 8,
+         rng.uniform(-0.5, 0.5, 200), 39.9),
+        ('fhn_pde_d512_rk8', lambda dn: O.System('fhn_pde', nx=16, mn=-1, mx=1, dense=dn), 8,
+         rng.uniform(-0.5, 0.5, 512), 425.0),
+    ]
+    res = {}
+    for name, mk, order, u0, ref in cases:
+        for dense in ((False, True) if name.startswith(('burgers', 'fhn')) else (False,)):
+            s = mk(dense)
+            U = u0.reshape(1, -1)
+            probe = 8
+            t0 = time.perf_counter()
+            s.rk_batch(order, [0.0], [1e-3 * probe], probe, U, nthreads=1)
+            per = (time.perf_counter() - t0) / probe
+            steps = int(max(probe, min(2_000_000, budget_s / max(per, 1e-9))))
+            t0 = time.perf_counter()
+            s.rk_batch(order, [0.0], [1e-3 * steps], steps, U, nthreads=1)
+            us = (time.perf_counter() - t0) / steps * 1e6
+            key = name + ('_dense' if dense else ('_stencil' if name.startswith(('burgers', 'fhn')) else ''))
+            res[key] = {'us_per_step': us, 'steps_timed': steps, 'reference_us_per_step': ref,
+                        'reference_over_port': ref / us}
+    return res
+
+
+def cpu_baseline(steps_per_slice_full, n_slices, target_s=10.0):
+    """Oracle C restatement (OpenMP over slices) on a bounded sample of the fine sweep."""
+    O = _oracle()
+    threads = cpu_threads()
     s = O.System('hopf', param=(500.0,))
     rng = np.random.default_rng(1234)
     U = rng.uniform(-0.5, 0.5, size=(n_slices, 3))
@@ -212,34 +338,32 @@ def cpu_baseline(steps_per_slice_full, n_slices, target_s=10.0):
     dt = time.perf_counter() - t0
     return {'value': n_slices * steps / dt, 'unit': 'fine RK steps/s', 'cores': threads, 'kind': 'port',
             'sample': f'{n_slices} Hopf slices x {steps} RK4 steps (of {steps_per_slice_full}), '
-                      f'{dt:.1f} s, oracle/nngp_oracle.c -O2 OpenMP'}
+                      f'{dt:.1f} s, oracle/nngp_oracle.c gcc -O3 -march=x86-64-v4 OpenMP',
+            'cpu_model': cpu_model()}
 
 
-def burgers_iter1(torch, g):
-    """GPU: the first nnGParareal iteration (fine sweep + 127 sequential corrections) of the
-    Burgers N=128 config, wall-clock (the CPU leg below times the same iteration)."""
-    ode = g.Burgers(d_x=128, normalization='-11')
-    solver = g.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
-    p = g.Parareal(ode, solver, [0, 5], 128, epsilon=5e-7, verbose=None)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    r = p.run(model='nngp', nn=15, seed=45, early_stop=1)
-    torch.cuda.synchronize()
-    return time.perf_counter() - t0, r
-
-
-def burgers_cpu_iter1(threads):
-    """CPU baseline for the north star's Burgers target: the oracle's C restatement (OpenMP over
-    slices for F and over the 1 152 fits of each correction) runs the same first iteration."""
-    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
-    import oracle as O
-    s = O.System('burgers', d=128, param=(0.01,), mn=0.0, mx=1.0)
+def burgers_cpu_converge(threads):
+    """CPU baseline for the north star's Burgers target, measured to convergence: the oracle's C
+    restatement runs the whole nnGParareal solve of the same config (OpenMP over slices for F and
+    over the 1 152 fits of each correction), F in the reference's dense formulation (Dxx@u,
+    Dx@u as 128 x 128 matrices, systems.py:421-446; bit-identical to the stencil).  Returns
+    (wall s, F s, result)."""
+    O = _oracle()
+    s = O.System('burgers', d=128, param=(0.01,), mn=0.0, mx=1.0, dense=True)
     x = np.linspace(-1, 1, 128)
     u0 = s.fit(0.5 * (np.cos(4.5 * np.pi * x) + 1))
+    f_time = [0.0]
+    rk_batch = s.rk_batch
+
+    def timed(*a, **k):
+        t = time.perf_counter()
+        out = rk_batch(*a, **k)
+        f_time[0] += time.perf_counter() - t
+        return out
+    s.rk_batch = timed
     t0 = time.perf_counter()
-    r = O.parareal(s, [0, 5], 128, 4, 2000, 'RK1', 'RK8', model='nngp', nn=15, seed=45, u0=u0,
-                   nthreads=threads, early_stop=1)
-    return time.perf_counter() - t0, r
+    r = O.parareal(s, [0, 5], 128, 4, 2000, 'RK1', 'RK8', model='nngp', nn=15, seed=45, u0=u0, nthreads=threads)
+    return time.perf_counter() - t0, f_time[0], r
 
 
 def burgers_published_schedule(torch, g, sample_pages=2):
@@ -364,14 +488,126 @@ def fhn_pde_fine_sweeps(torch, g):
     return res
 
 
+def fhn_strong(torch, g, world, rank, steps=3, warmup=1, sample=400, n_pred=4):
+    """The north star's strong-scaling workload, FHN-PDE d=800 (d_x=20), N=512 slices, at every
+    world size: the fine sweep of all 512 slices sharded into contiguous blocks (512/world per
+    rank, fine_sweep_sharded) + the all-gather of the end states, and the nnGP correction of one
+    slice with its 7 200 fits sharded by coordinate (nngp_predict_range, 800/world coordinates
+    per rank) + the all-gather of the predictions.  Timed between barriers, max over ranks.
+    Projected iteration = F (195 325 RK8 steps per slice, FHN_PDE.py's 1e8 schedule) + 511
+    corrections.  At world = 1 the 8-GPU per-rank shares are also measured on this GPU (64
+    slices; 100 of the 800 coordinates), giving the projected 1 -> 8 speed-up."""
+    import ctypes
+    from nngp_amd.models import JITTERS
+    from nngp_amd.parareal import shard_bounds
+    dist = torch.distributed
+    n_sl, nx = 512, 20
+    d = 2 * nx * nx
+    steps_it = 195325
+    ode = g.FHN_PDE(d_x=nx)
+    solver = g.SolverRK(ode.get_vector_field(), Ng=50, Nf=sample, F='RK8', G='RK4', thresh=float('inf'))
+    dev = lambda a: torch.tensor(a, dtype=torch.float64, device='cuda')
+    rng = np.random.default_rng(0)
+    t = np.linspace(0, 1100, n_sl + 1)
+    U = np.clip(ode.get_init_cond()[None, :] + 0.01 * rng.standard_normal((n_sl, d)), -1, 1)
+    Ud, td = dev(U), dev(t)
+    UF = torch.empty((n_sl + 1, d), dtype=torch.float64, device='cuda')
+    Ufull = torch.empty((n_sl + 1, d), dtype=torch.float64, device='cuda')
+    Ufull[:n_sl] = Ud
+    group = None if world > 1 else None
+    prop = lambda a, b, u, out: solver.run_F_batch(a, b, u, out=out)
+
+    def sweep():
+        if world > 1:
+            g.parareal.fine_sweep_sharded(prop, td, Ufull, UF, 0, n_sl, group)
+        else:
+            solver.run_F_batch(td[:-1], td[1:], Ud, out=UF[1:])
+
+    def timed(fn, k):
+        barrier_sync(torch, world)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        barrier_sync(torch, world)
+        el = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([el], dtype=torch.float64, device='cuda')
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        return el / k
+
+    for _ in range(warmup):
+        sweep()
+    f_s = timed(sweep, steps)
+    # nnGP correction of one slice, coordinate-sharded over the ranks (same data on every rank)
+    rows, m = 3000, 20
+    X = np.clip(np.cumsum(0.01 * rng.standard_normal((rows, d)), axis=0), -1, 1)
+    Y = 0.02 * np.sin(2 * X)
+    mdl = g.NNGP_p(n=d, N=4, nn=m, n_restarts=1, seed=45)
+    th0 = dev(mdl.draw_thetas(1))
+    Xd, Yd = dev(X), dev(Y)
+    jit = np.ascontiguousarray(JITTERS)
+    jp = jit.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    lib = g.lib()
+    c0, c1, chunk = shard_bounds(0, d, world, rank)
+    send = torch.zeros(chunk, dtype=torch.float64, device='cuda')
+    qs = [Xd[(97 * j) % rows] + 1e-3 for j in range(n_pred)]
+    st = torch.cuda.current_stream().cuda_stream
+
+    def range_pred(q, a, b, out):
+        g._lib.check(lib.nngp_predict_range(Xd.data_ptr(), Yd.data_ptr(), rows, d, q.data_ptr(), m, len(jit), jp, 1,
+                                            th0.data_ptr(), a, b, 0.1, 0.1, 400, out.data_ptr(), st))
+
+    def corrections():
+        for q in qs:
+            if c1 > c0:
+                range_pred(q, c0, c1, send[:c1 - c0])
+            if world > 1:
+                g.parareal._all_gather_flat(send, None, world)
+
+    corrections()
+    c_s = timed(corrections, 1) / n_pred
+    res = {'workload': 'FHN-PDE d=800 (d_x=20) N=512, RK8 fine sweep + coordinate-sharded nnGP corrections (m=20)',
+           'world': world, 'slices_per_rank': (n_sl + world - 1) // world,
+           'F_us_per_step': f_s / sample * 1e6, 'F_steps_per_s': n_sl * sample / f_s,
+           'correction_ms': c_s * 1e3, 'corrections_per_s': 1 / c_s,
+           'iteration_s_projected': f_s / sample * steps_it + (n_sl - 1) * c_s,
+           'sample': f'{sample} RK8 steps x 512 slices; {n_pred} corrections of 7200 fits (rows {rows})'}
+    if world == 1:   # the 8-GPU per-rank shares, measured on this GPU
+        sh = 64
+        sweep8 = lambda: solver.run_F_batch(td[:sh], td[1:sh + 1], Ud[:sh].contiguous(), out=UF[1:sh + 1])
+        sweep8()
+        f8 = timed(sweep8, steps)
+        out8 = torch.empty(100, dtype=torch.float64, device='cuda')
+
+        def corr8():
+            for q in qs:
+                range_pred(q, 0, 100, out8)
+        corr8()
+        c8 = timed(corr8, 1) / n_pred
+        it1 = res['iteration_s_projected']
+        it8 = f8 / sample * steps_it + (n_sl - 1) * c8
+        res['per_rank_share_8gpu'] = {'F_us_per_step_64_slices': f8 / sample * 1e6,
+                                      'correction_ms_100_coords': c8 * 1e3,
+                                      'iteration_s_projected_8gpu': it8,
+                                      'projected_speedup_1_to_8': it1 / it8,
+                                      'projected_F_speedup_1_to_8': f_s / f8,
+                                      'note': 'excludes the per-iteration all-gather (3.3 MB) and the '
+                                              'per-slice all-gather of 800 predictions (6.4 KB)'}
+    return res
+
+
 def read_traffic():
+    """HBM bytes per launch of the fine kernel from the committed PMC passes (tools/pmc_traffic.py:
+    the median over the profiled launches, with the max beside it)."""
     path = os.path.join(ROOT, 'profiles', 'fine_kernel_traffic.json')
     if os.path.exists(path):
         try:
-            return json.load(open(path)).get('bytes_per_launch')
+            t = json.load(open(path))
+            return t.get('bytes_per_launch'), t.get('bytes_per_launch_max')
         except Exception:
-            return None
-    return None
+            return None, None
+    return None, None
 
 
 def main():
@@ -382,6 +618,10 @@ def main():
     ap.add_argument('--steps-per-slice', type=int, default=2048 * 85 * 10000 // 128)   # 13.6e6
     ap.add_argument('--slices-per-gpu', type=int, default=128)
     ap.add_argument('--no-extras', action='store_true', help='skip corrections/convergence/CPU legs')
+    ap.add_argument('--workload', choices=['hopf', 'fhn_pde'], default='hopf',
+                    help="headline value: 'hopf' = BASELINE configs[1] Hopf fine sweep, weak scaling "
+                         "(128 slices per GPU); 'fhn_pde' = FHN-PDE d=800 N=512 fine sweep, strong "
+                         "scaling (512 slices over all GPUs; the north star's 1->8 target)")
     args = ap.parse_args()
 
     import torch
@@ -395,6 +635,7 @@ def main():
     value = total_steps / elapsed
     flops_launch = FLOPS_PER_STEP[('hopf', 'RK4')] * args.steps_per_slice * args.slices_per_gpu
     achieved_tf = flops_launch / kernel_s / 1e12
+    traffic, traffic_max = read_traffic()
     res = {
         'metric': 'fine RK steps/sec (+ nnGP corrections/sec; wall-clock to convergence)',
         'value': value, 'unit': 'fine RK steps/s', 'n_gpus': world, 'steps': args.steps,
@@ -404,7 +645,10 @@ def main():
                    'slices_per_gpu': args.slices_per_gpu, 'total_slices': n_total,
                    'steps_per_slice': args.steps_per_slice, 'parallelism': f'time-slices x{world}'},
         'roofline': {'bound': 'fp64-valu', 'achieved': achieved_tf, 'peak': FP64_PEAK_TFLOPS,
-                     'unit': 'TFLOP/s', 'frac': achieved_tf / FP64_PEAK_TFLOPS, 'traffic': read_traffic(),
+                     'unit': 'TFLOP/s', 'frac': achieved_tf / FP64_PEAK_TFLOPS, 'traffic': traffic,
+                     'traffic_max': traffic_max,
+                     'hbm_GBps': (traffic / kernel_s / 1e9) if traffic else None, 'hbm_peak_GBps': HBM_PEAK_GBS,
+                     'algorithmic_bytes_per_launch': args.slices_per_gpu * (2 * 3 * 8 + 2 * 8),
                      'kernel': 'rk_group_kernel<HOPF,RK4>', 'kernel_ms': kernel_s * 1e3,
                      'issue_floor_us_per_step': LANE_VALU_PER_STEP * CYCLES_PER_F64_VALU / (SHADER_GHZ * 1e3),
                      'us_per_step': kernel_s / args.steps_per_slice * 1e6,
@@ -412,20 +656,43 @@ def main():
                                          / (kernel_s / args.steps_per_slice),
                      'flops_per_step_per_slice': FLOPS_PER_STEP[('hopf', 'RK4')]},
     }
+    # the strong-scaling workload (FHN-PDE N=512), measured at every world size
+    strong = fhn_strong(torch, g, world, rank)
+    res['fhn_pde_strong'] = strong
+    if args.workload == 'fhn_pde':
+        res.update({'value': strong['F_steps_per_s'], 'scaling': 'strong',
+                    'ms_per_step': strong['F_us_per_step'] * 400 / 1e3,
+                    'config': {'workload': strong['workload'], 'total_slices': 512, 'd': 800,
+                               'slices_per_gpu': strong['slices_per_rank'], 'parallelism': f'time-slices x{world}'}})
     if rank == 0 and world == 1 and not args.no_extras:
         n_pred, pred_s, _ = corrections_bench(torch, g)
         res['nngp_corrections_per_s'] = n_pred / pred_s
         res['nngp_correction_ms'] = pred_s / n_pred * 1e3
+        runs = {}
         for which in ('burgers', 'hopf'):
-            wall, k, conv, tim = converge(torch, g, which)
+            wall, k, conv, tim, runs[which] = converge(torch, g, which)
             res[f'{which}_n128_to_convergence'] = {'wall_s': wall, 'K': k, 'converged': conv,
                                                    'F_time_s': tim['F_time'], 'mdl_time_s': tim['mdl_tot_t'],
                                                    'conv_int': tim.get('conv_int', []),
                                                    'spec_hits': tim.get('spec_hits', [])}
             log(which, 'converged', conv, 'K', k, f'{wall:.2f}s')
         res['nngp_corrections_fhn_d200'] = corrections_fhn_d200(torch, g)
+        res['nngp_correction_roofline'] = {f'd{d}_m{m}_R{R}': correction_roofline(torch, g, d, m, R)
+                                           for d, m, R in ((800, 20, 1), (200, 20, 1), (128, 15, 1), (3, 15, 2))}
+        log('correction roofline', json.dumps(res['nngp_correction_roofline']))
         res['nngp_corrections_hopf_vs_reference'] = {'reference_corrections_per_s_141_cores': 44.0,
                                                       'ratio': res['nngp_corrections_per_s'] / 44.0}
+        res['fhn_pde_n512_to_convergence'] = fhn_pde_converge(torch, g)
+        log('fhn-pde d=800 N=512', json.dumps(res['fhn_pde_n512_to_convergence']))
+        # the published FHN-PDE run at d_x = 16 (FHN_PDE.py:27-181, FHN_scal_times_16_512_nngp):
+        # G = RK4 25 steps/slice as published; reference K = 6 in 17 849 s on 517 cores
+        r16 = fhn_pde_converge(torch, g, dx=16, ng=25)
+        r16.update({'reference_K': 6, 'reference_wall_s_517_cores': 17849.0,
+                    'speedup_vs_reference_wall': 17849.0 / r16['wall_s'],
+                    'note': 'F unpaged here (195 325 RK8 steps/slice); the published run paged it 25x '
+                            '(4.9e6 effective steps/slice, SURVEY.md 0.4), so its F time is ~25x ours'})
+        res['fhn_pde_d512_n512_published_config'] = r16
+        log('fhn-pde d=512 N=512 published', json.dumps(r16))
         res['gparareal_lorenz_n32'] = gparareal_lorenz(torch, g)
         log('gparareal lorenz K', res['gparareal_lorenz_n32']['K'], f"{res['gparareal_lorenz_n32']['wall_s']:.2f}s")
         res['burgers_n128_published_schedule'] = burgers_published_schedule(torch, g)
@@ -433,24 +700,22 @@ def main():
         res['hopf_n128_published_schedule'] = hopf_published_schedule(torch, g)
         res['fhn_pde_n512_fine_sweep'] = fhn_pde_fine_sweeps(torch, g)
         res['cpu_baseline'] = cpu_baseline(args.steps_per_slice, args.slices_per_gpu)
-        # north-star target (>= 10x the CPU path on Burgers N=128, identical K): time the first
-        # iteration on both sides and extrapolate the CPU to the GPU run's K
-        g_s, g_r = burgers_iter1(torch, g)
-        c_s, c_r = burgers_cpu_iter1(res['cpu_baseline']['cores'])
-        same = bool(np.array_equal(np.nan_to_num(g_r['u'], nan=7.0), np.nan_to_num(c_r['u'], nan=7.0)))
+        res['cpu_single_core'] = cpu_single_core()
+        log('cpu single core', json.dumps(res['cpu_single_core']))
+        # north-star target (>= 10x the CPU path on Burgers N=128, identical K): the CPU
+        # restatement runs the same nnGParareal solve to convergence, measured (not extrapolated)
+        c_s, c_f, c_r = burgers_cpu_converge(res['cpu_baseline']['cores'])
+        g_r = runs['burgers']
         conv = res['burgers_n128_to_convergence']
-        # CPU cost of an iteration ~ its N-I corrections: extrapolate iteration 1 by the run's own
-        # per-iteration correction counts (conv_int of the GPU run, whose iterates are bitwise the
-        # oracle's)
-        preds = [128 - 1] + [128 - c - 1 for c in conv['conv_int'][:-1]]
-        cpu_est = c_s * sum(preds) / preds[0]
+        same = bool(np.array_equal(np.nan_to_num(g_r['u'], nan=7.0), np.nan_to_num(c_r['u'], nan=7.0)))
         res['burgers_n128_vs_cpu'] = {
-            'gpu_iter1_s': g_s, 'cpu_iter1_s': c_s, 'iter1_speedup': c_s / g_s,
-            'iter1_bitwise_equal': same, 'cpu_cores': res['cpu_baseline']['cores'],
-            'cpu_to_convergence_est_s': cpu_est, 'gpu_to_convergence_s': conv['wall_s'],
-            'speedup_to_convergence_est': cpu_est / conv['wall_s'], 'K': conv['K'],
-            'note': 'CPU = oracle C restatement (OpenMP), first Parareal iteration of the same run, '
-                    'extrapolated to the run by its per-iteration correction counts'}
+            'gpu_to_convergence_s': conv['wall_s'], 'cpu_to_convergence_s': c_s,
+            'speedup_to_convergence': c_s / conv['wall_s'], 'K_gpu': conv['K'], 'K_cpu': c_r['k'],
+            'iterates_bitwise_equal': same, 'cpu_F_s': c_f, 'cpu_cores': res['cpu_baseline']['cores'],
+            'cpu_model': cpu_model(),
+            'note': 'CPU = oracle C restatement (gcc -O3 -march=x86-64-v4, OpenMP over slices and fits), '
+                    'F in the reference dense formulation; the whole run to convergence on both sides'}
+        log('burgers cpu', json.dumps(res['burgers_n128_vs_cpu']))
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -441,7 +441,8 @@ __global__ void __launch_bounds__(256) d2_kernel(const double *__restrict__ xm, 
 //     the transposed L read back from the same LDS image.
 // Arithmetic order (restated in oracle/nngp_oracle.c gp_factor / butterfly_sum):
 //   K_rj = psy*exp(c*D2_rj) (+ jit on the diagonal)                 models.py:146-155, 88
-//   L_ij = (((K_ij - L_i0 L_j0) - L_i1 L_j1) - ...) * RN(1/L_jj)      potrf, k ascending
+//   L_ij = (K_ij - sum_k L_ik L_jk) * RN(1/L_jj), the sums in OpenBLAS dpotf2_L's order (ddot
+//          for the pivot, dgemv_n's 4-column fma blocks / tail-row fma chain below; gp_factor)
 //   z, alpha: successive subtraction, k ascending / descending; x/L_ii as Markstein x*RN(1/L_ii)
 //   sums over rows: lane pairs (l, l+16) first, then butterfly levels 1, 2, 4, 8
 // ---------------------------------------------------------------------------------------------
@@ -606,19 +607,53 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
         diag[s] = 1.0;
         rinv[s] = 1.0;
     }
+    // OpenBLAS dpotf2_L's sums (the reference's LAPACK; oracle potf2_dot / potf2_gemv_row):
+    //   pivot   a_jj - ddot(row j): accumulators t1/t2 over groups of 4, fma(x0,x0,x2^2) etc.;
+    //   below   "vector rows" (the first ((m-1-j) & -4) rows under j): y -= 4-column fma chains,
+    //           leftover columns y -= a*x; "tail rows" (the last (m-1-j) & 3): y -= one fma chain.
+    //   Each lane evaluates both row forms (their operation counts add up to the old successive
+    //   subtraction's) and keeps the one its row takes.
     static_for<0, MAXM>([&](auto jc) {
         constexpr int j = decltype(jc)::value, SJ = j / 16, LJ = j % 16;
-        double t[RPL];
+        const int tail_start = j + 1 + ((m - 1 - j) & ~3);
+        double yv[RPL], tt[RPL], blk[RPL];
 #pragma unroll
         for (int s = 0; s < RPL; s++)
-            if (16 * (s + 1) > j) t[s] = a[s][j];
+            if (16 * (s + 1) > j) {
+                yv[s] = a[s][j];
+                tt[s] = 0.0;
+                blk[s] = 0.0;
+            }
+        double d1 = 0.0, d2 = 0.0;   // the pivot row's ddot (row j lives in set SJ, lane LJ)
 #pragma unroll
         for (int k = 0; k < j; k++) {
             const double ljk = row_bcast<LJ>(a[SJ][k]);
 #pragma unroll
             for (int s = 0; s < RPL; s++)
-                if (16 * (s + 1) > j) t[s] = t[s] - a[s][k] * ljk;
+                if (16 * (s + 1) > j) {
+                    const double ak = a[s][k];
+                    if (k < (j & ~3)) {   // whole 4-column blocks of the vector-row form
+                        blk[s] = (k % 4 == 0) ? ak * ljk : fma(ak, ljk, blk[s]);
+                        if (k % 4 == 3) yv[s] = yv[s] - blk[s];
+                    } else {
+                        yv[s] = yv[s] - ak * ljk;
+                    }
+                    tt[s] = fma(ak, ljk, tt[s]);
+                }
+            // pivot ddot over the row-j owner's own entries L_jk (its set SJ)
+            const double xk = a[SJ][k];
+            if (k < (j & ~3)) {
+                if (k % 4 == 2) d1 = d1 + fma(a[SJ][k - 2], a[SJ][k - 2], xk * xk);
+                if (k % 4 == 3) d2 = d2 + fma(a[SJ][k - 2], a[SJ][k - 2], xk * xk);
+            } else {
+                d1 = fma(xk, xk, d1);
+            }
         }
+        double t[RPL];
+#pragma unroll
+        for (int s = 0; s < RPL; s++)
+            if (16 * (s + 1) > j) t[s] = (l + 16 * s >= tail_start) ? a[s][j] - tt[s] : yv[s];
+        t[SJ] = (l == LJ) ? a[SJ][j] - (d1 + d2) : t[SJ];
         const double piv = row_bcast<LJ>(t[SJ]);
         fail = fail || !(piv > 0.0);
         const double ljj = sqrt(piv);

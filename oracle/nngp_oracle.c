@@ -26,7 +26,8 @@
  * GPU-vs-oracle parity is (near) bitwise and oracle-vs-reference is within a stated tolerance:
  *   - sum over d of squared differences in the GP kernel: numpy pairwise_sum order
  *   - kNN distance: sequential (scipy cdist sqeuclidean, transform_reduce_2d_)
- *   - Cholesky: left-looking, successive subtraction, scale by reciprocal (OpenBLAS potf2)
+ *   - Cholesky: OpenBLAS dpotf2_L's structure (pivot = a_jj - ddot, column = dgemv_n then scale by
+ *     the reciprocal; the kernels' accumulation order, see potf2_dot / potf2_gemv_row)
  *   - triangular solves: successive subtraction (OpenBLAS trsv column sweeps)
  *   - y^T alpha, sum(log diag L), K*^T alpha: per lane l the rows l, l+16, l+32, l+48 summed
  *     left to right, then a balanced binary tree over the 16 lanes, = the GPU's xor-butterfly
@@ -117,19 +118,18 @@ static void burgers_rhs(int d, double nu, const double *u, double *out) {
     const double cxx = nu / (dx * dx);      /* Dxx = (nu/dx^2) * Txx                       */
     const double cdg = cxx * -2.0;          /* diagonal entry                              */
     const double q = 1.0 / (2 * dx);        /* Dx = (1/(2 dx)) * Tx                        */
-    for (int i = 0; i < d; i++) {
-        double lap, grad;
-        if (i == 0) {
-            lap = (cdg * u[0] + cxx * u[1]) + cxx * u[d - 1];
-            grad = q * u[1] + (-q) * u[d - 1];
-        } else if (i == d - 1) {
-            lap = (cxx * u[0] + cxx * u[d - 2]) + cdg * u[d - 1];
-            grad = q * u[0] + (-q) * u[d - 2];
-        } else {
-            lap = (cxx * u[i - 1] + cdg * u[i]) + cxx * u[i + 1];
-            grad = (-q) * u[i - 1] + q * u[i + 1];
-        }
-        out[i] = lap - u[i] * grad; /* Dxx@u - u*(Dx@u), systems.py:446 */
+    {   /* row 0: columns 0, 1, d-1; row d-1: columns 0, d-2, d-1 */
+        const double lap0 = (cdg * u[0] + cxx * u[1]) + cxx * u[d - 1];
+        const double grad0 = q * u[1] + (-q) * u[d - 1];
+        const double lapn = (cxx * u[0] + cxx * u[d - 2]) + cdg * u[d - 1];
+        const double gradn = q * u[0] + (-q) * u[d - 2];
+        out[0] = lap0 - u[0] * grad0;   /* Dxx@u - u*(Dx@u), systems.py:446 */
+        out[d - 1] = lapn - u[d - 1] * gradn;
+    }
+    for (int i = 1; i < d - 1; i++) {
+        const double lap = (cxx * u[i - 1] + cdg * u[i]) + cxx * u[i + 1];
+        const double grad = (-q) * u[i - 1] + q * u[i + 1];
+        out[i] = lap - u[i] * grad;
     }
 }
 
@@ -178,11 +178,124 @@ static void fhn_pde_rhs(int nx, const double *u, double *out) {
     for (int y = 0; y < nx; y++)
         for (int x = 0; x < nx; x++) {
             const int i = y * nx + x;
-            const double lu = fhn_lap_row(nx, ad, ax, ay, u1, y, x);
-            const double lv = fhn_lap_row(nx, bd, bx, by, u2, y, x);
+            double lu, lv;
+            if (y > 0 && y < nx - 1 && x > 0 && x < nx - 1) {   /* no wrap: columns already ascending */
+                lu = (((ay * u1[i - nx] + ax * u1[i - 1]) + ad * u1[i]) + ax * u1[i + 1]) + ay * u1[i + nx];
+                lv = (((by * u2[i - nx] + bx * u2[i - 1]) + bd * u2[i]) + bx * u2[i + 1]) + by * u2[i + nx];
+            } else {
+                lu = fhn_lap_row(nx, ad, ax, ay, u1, y, x);
+                lv = fhn_lap_row(nx, bd, bx, by, u2, y, x);
+            }
             out[i] = (((lu + u1[i]) - cube(u1[i])) - u2[i]) + k * 1.0;
             out[h + i] = itau * ((lv + u1[i]) - u2[i]);
         }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* The reference's DENSE formulation of the PDE fields (the timed "reference formulation" CPU  */
+/* leg): Burgers Dxx@u - u*(Dx@u) with the d x d matrices (systems.py:421-446),  */
+/* FHN-PDE (a(DXX+DYY))@u1, (b(DXX+DYY))@u2 with the h x h Laplacian (systems.py:321-368), as    */
+/* XLA evaluates them: every matrix entry multiplied, zeros included.  Each y_i is summed over   */
+/* j ascending (column sweeps, vectorised across i without reassociation), so the non-zero      */
+/* terms add in the stencil's order and the result equals the stencil RHS bit for bit (up to the */
+/* sign of an exact zero); only the cost differs: 2d^2 (Burgers) / h^2 per matvec.              */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+    int n;             /* matrix order: d (Burgers), h = nx^2 (FHN-PDE)                          */
+    double *A1T, *A2T; /* column-major: Dxx, Dx (Burgers) / a*L, b*L (FHN-PDE)                   */
+} dense_ctx;
+
+static void dense_free(dense_ctx *c) {
+    if (!c) return;
+    free(c->A1T);
+    free(c->A2T);
+    free(c);
+}
+
+static dense_ctx *dense_build(const nngp_system *sys) {
+    dense_ctx *c = (dense_ctx *)calloc(1, sizeof(dense_ctx));
+    if (!c) return NULL;
+    if (sys->kind == NNGP_SYS_BURGERS) {
+        const int d = sys->d;
+        const double dx = (1.0 - (-1.0)) / (d - 1), nu = sys->param[0];
+        const double cxx = nu / (dx * dx), q = 1.0 / (2 * dx);
+        c->n = d;
+        c->A1T = (double *)calloc((size_t)d * d, sizeof(double));
+        c->A2T = (double *)calloc((size_t)d * d, sizeof(double));
+        if (!c->A1T || !c->A2T) { dense_free(c); return NULL; }
+#define AT(M, i, j) (M)[(size_t)(j) * d + (i)]
+        for (int i = 0; i < d; i++) {       /* Txx: -2 diagonal, 1 off; Tx: +1 above, -1 below */
+            AT(c->A1T, i, i) = cxx * -2.0;
+            if (i + 1 < d) {
+                AT(c->A1T, i, i + 1) = cxx * 1.0;
+                AT(c->A1T, i + 1, i) = cxx * 1.0;
+                AT(c->A2T, i, i + 1) = q * 1.0;
+                AT(c->A2T, i + 1, i) = q * -1.0;
+            }
+        }
+        AT(c->A1T, 0, d - 1) = 1 * cxx;      /* periodic corners, Burgers.py:53-56 / systems.py */
+        AT(c->A1T, d - 1, 0) = 1 * cxx;
+        AT(c->A2T, 0, d - 1) = -1 * q;
+        AT(c->A2T, d - 1, 0) = 1 * q;
+#undef AT
+    } else if (sys->kind == NNGP_SYS_FHN_PDE) {
+        const int nx = sys->nx, h = nx * nx;
+        const double dx = (1.0 - (-1.0)) / (nx - 1);
+        const double c1 = 1 / (dx * dx);
+        const double ldiag = c1 * -2.0 + c1 * -2.0;
+        const double a = 2.8E-4, b = 5E-3;
+        c->n = h;
+        c->A1T = (double *)calloc((size_t)h * h, sizeof(double));
+        c->A2T = (double *)calloc((size_t)h * h, sizeof(double));
+        if (!c->A1T || !c->A2T) { dense_free(c); return NULL; }
+        for (int y = 0; y < nx; y++)
+            for (int x = 0; x < nx; x++) {
+                const int i = y * nx + x;
+                const int ym = (y == 0) ? nx - 1 : y - 1, yp = (y == nx - 1) ? 0 : y + 1;
+                const int xm = (x == 0) ? nx - 1 : x - 1, xp = (x == nx - 1) ? 0 : x + 1;
+                const int cols[4] = {ym * nx + x, y * nx + xm, y * nx + xp, yp * nx + x};
+                c->A1T[(size_t)i * h + i] = a * ldiag;
+                c->A2T[(size_t)i * h + i] = b * ldiag;
+                for (int t = 0; t < 4; t++) {
+                    c->A1T[(size_t)cols[t] * h + i] = a * c1;
+                    c->A2T[(size_t)cols[t] * h + i] = b * c1;
+                }
+            }
+    } else {
+        dense_free(c);
+        return NULL;
+    }
+    return c;
+}
+
+/* y = A x, y_i = sum_j A_ij x_j over j ascending (AT column-major)                           */
+static void matvec_cols(int n, const double *restrict AT, const double *restrict x, double *restrict y) {
+    const double x0 = x[0];
+    for (int i = 0; i < n; i++) y[i] = AT[i] * x0;
+    for (int j = 1; j < n; j++) {
+        const double xj = x[j];
+        const double *restrict col = AT + (size_t)j * n;
+        for (int i = 0; i < n; i++) y[i] = y[i] + col[i] * xj;
+    }
+}
+
+static void rhs_dense(const nngp_system *sys, const dense_ctx *c, const double *u, double *out) {
+    const int n = c->n;
+    double *y1 = (double *)__builtin_alloca(sizeof(double) * 2 * (size_t)n), *y2 = y1 + n;
+    if (sys->kind == NNGP_SYS_BURGERS) {
+        matvec_cols(n, c->A1T, u, y1);
+        matvec_cols(n, c->A2T, u, y2);
+        for (int i = 0; i < n; i++) out[i] = y1[i] - u[i] * y2[i];   /* systems.py:446 */
+    } else {
+        const double *u1 = u, *u2 = u + n;
+        const double k = -5E-3, itau = 1 / 0.1;
+        matvec_cols(n, c->A1T, u1, y1);
+        matvec_cols(n, c->A2T, u2, y2);
+        for (int i = 0; i < n; i++) {
+            out[i] = (((y1[i] + u1[i]) - cube(u1[i])) - u2[i]) + k * 1.0;
+            out[n + i] = itau * ((y2[i] + u1[i]) - u2[i]);
+        }
+    }
 }
 
 static void rhs_raw(const nngp_system *sys, const double *u, double *out) {
@@ -245,16 +358,23 @@ static void rhs_raw(const nngp_system *sys, const double *u, double *out) {
 }
 
 /* systems.py:36-40 + utils.py:24,31: f_n(u) = f(inverse(u)) * scale                         */
-void orc_rhs(const nngp_system *sys, const double *u, double *out, double *scratch) {
+static void rhs_ex(const nngp_system *sys, const dense_ctx *dc, const double *u, double *out, double *scratch) {
     const int d = sys->d;
-    if (!sys->normalized) {
-        rhs_raw(sys, u, out);
-        return;
+    if (sys->normalized) {
+        const double *mn = sys->norm, *w = sys->norm + d;
+        for (int i = 0; i < d; i++) scratch[i] = ((u[i] + 1) / 2) * w[i] + mn[i];
+        u = scratch;
     }
-    const double *mn = sys->norm, *w = sys->norm + d, *sc = sys->norm + 2 * d;
-    for (int i = 0; i < d; i++) scratch[i] = ((u[i] + 1) / 2) * w[i] + mn[i];
-    rhs_raw(sys, scratch, out);
-    for (int i = 0; i < d; i++) out[i] = out[i] * sc[i];
+    if (dc) rhs_dense(sys, dc, u, out);
+    else rhs_raw(sys, u, out);
+    if (sys->normalized) {
+        const double *sc = sys->norm + 2 * d;
+        for (int i = 0; i < d; i++) out[i] = out[i] * sc[i];
+    }
+}
+
+void orc_rhs(const nngp_system *sys, const double *u, double *out, double *scratch) {
+    rhs_ex(sys, NULL, u, out, scratch);
 }
 
 /* ------------------------------------------------------------------------------------------ */
@@ -262,8 +382,8 @@ void orc_rhs(const nngp_system *sys, const double *u, double *out, double *scrat
 /* ------------------------------------------------------------------------------------------ */
 /* general form: FIXED uses h = (t1-t0)/steps; LINSPACE walks steps j0..j0+steps-1 of the grid
  * np.linspace(t0, t1, gsteps+1) (gsteps = steps, j0 = 0: the per-slice grid of RK.run)     */
-int orc_rk_grid(const nngp_system *sys, int order, int mode, double t0, double t1, int64_t gsteps,
-                int64_t j0, int64_t steps, const double *u0, double *u1) {
+static int rk_core(const nngp_system *sys, const dense_ctx *dc, int order, int mode, double t0, double t1,
+                   int64_t gsteps, int64_t j0, int64_t steps, const double *u0, double *u1) {
     tableau_t T;
     make_tableau(order, &T);
     const int d = sys->d, S = T.S;
@@ -284,37 +404,75 @@ int orc_rk_grid(const nngp_system *sys, int order, int mode, double t0, double t
             h = tn1 - tn;
         }
         /* k_0 = h*f(u); k_i = h*f(u + sum_{j<i} a_ij k_j)                                  */
-        orc_rhs(sys, u, k, scr);
+        rhs_ex(sys, dc, u, k, scr);
         for (int c = 0; c < d; c++) k[c] = h * k[c];
         for (int i = 1; i < S; i++) {
             /* the reference sums from temp = 0 (RK.py:153-166); starting from the first non-zero
-             * term is identical up to the sign of an exact zero (the HIP kernels do the same)    */
-            for (int c = 0; c < d; c++) {
-                double t = 0.0;
-                int first = 1;
-                for (int j = 0; j < i; j++) {
-                    if (T.a[i][j] == 0.0) continue;
-                    const double v = T.a[i][j] * k[(size_t)j * d + c];
-                    t = first ? v : t + v;
-                    first = 0;
+             * term is identical up to the sign of an exact zero (the HIP kernels do the same).
+             * Each element's terms are added in ascending j; the loops run j outer, c inner so
+             * the per-element sums vectorise across c without reassociation.                   */
+            if (d <= 8) {   /* small systems: per-element scalar sums (same order) */
+                for (int c = 0; c < d; c++) {
+                    double t = 0.0;
+                    int first = 1;
+                    for (int j = 0; j < i; j++) {
+                        if (T.a[i][j] == 0.0) continue;
+                        const double v = T.a[i][j] * k[(size_t)j * d + c];
+                        t = first ? v : t + v;
+                        first = 0;
+                    }
+                    tmp[c] = first ? u[c] : u[c] + t;
                 }
-                tmp[c] = first ? u[c] : u[c] + t;
+                double *ki = k + (size_t)i * d;
+                rhs_ex(sys, dc, tmp, ki, scr);
+                for (int c = 0; c < d; c++) ki[c] = h * ki[c];
+                continue;
             }
+            int first = 1;
+            for (int j = 0; j < i; j++) {
+                const double a = T.a[i][j];
+                if (a == 0.0) continue;
+                const double *kj = k + (size_t)j * d;
+                if (first)
+                    for (int c = 0; c < d; c++) tmp[c] = a * kj[c];
+                else
+                    for (int c = 0; c < d; c++) tmp[c] = tmp[c] + a * kj[c];
+                first = 0;
+            }
+            if (first)
+                memcpy(tmp, u, sizeof(double) * d);
+            else
+                for (int c = 0; c < d; c++) tmp[c] = u[c] + tmp[c];
             double *ki = k + (size_t)i * d;
-            orc_rhs(sys, tmp, ki, scr);
+            rhs_ex(sys, dc, tmp, ki, scr);
             for (int c = 0; c < d; c++) ki[c] = h * ki[c];
         }
         /* u += sum_s b_s k_s  (jnp.sum(b*k,1); zeros in b are exact no-ops)                */
-        for (int c = 0; c < d; c++) {
-            double acc = 0.0;
+        if (d <= 8) {
+            for (int c = 0; c < d; c++) {
+                double acc = 0.0;
+                int first = 1;
+                for (int s2 = 0; s2 < S; s2++) {
+                    if (T.b[s2] == 0.0) continue;
+                    const double v = T.b[s2] * k[(size_t)s2 * d + c];
+                    acc = first ? v : acc + v;
+                    first = 0;
+                }
+                u[c] = u[c] + acc;
+            }
+        } else {
             int first = 1;
-            for (int s = 0; s < S; s++) {
-                if (T.b[s] == 0.0) continue;
-                const double v = T.b[s] * k[(size_t)s * d + c];
-                acc = first ? v : acc + v;
+            for (int s2 = 0; s2 < S; s2++) {
+                const double b = T.b[s2];
+                if (b == 0.0) continue;
+                const double *ks = k + (size_t)s2 * d;
+                if (first)
+                    for (int c = 0; c < d; c++) tmp[c] = b * ks[c];
+                else
+                    for (int c = 0; c < d; c++) tmp[c] = tmp[c] + b * ks[c];
                 first = 0;
             }
-            u[c] = u[c] + acc;
+            for (int c = 0; c < d; c++) u[c] = u[c] + tmp[c];
         }
     }
     memcpy(u1, u, sizeof(double) * d);
@@ -322,22 +480,39 @@ int orc_rk_grid(const nngp_system *sys, int order, int mode, double t0, double t
     return 0;
 }
 
-int orc_rk(const nngp_system *sys, int order, int mode, double t0, double t1, int64_t steps,
-           const double *u0, double *u1) {
-    return orc_rk_grid(sys, order, mode, t0, t1, steps, 0, steps, u0, u1);
+int orc_rk_grid(const nngp_system *sys, int order, int mode, double t0, double t1, int64_t gsteps,
+                int64_t j0, int64_t steps, const double *u0, double *u1) {
+    return rk_core(sys, NULL, order, mode, t0, t1, gsteps, j0, steps, u0, u1);
 }
 
-int orc_rk_batch(const nngp_system *sys, int order, int mode, int n_slices, const double *t0,
-                 const double *t1, int64_t steps, const double *u0, double *uF, int nthreads) {
+int orc_rk(const nngp_system *sys, int order, int mode, double t0, double t1, int64_t steps,
+           const double *u0, double *u1) {
+    return rk_core(sys, NULL, order, mode, t0, t1, steps, 0, steps, u0, u1);
+}
+
+/* dense != 0: the PDE fields in the reference's dense-matrix formulation (see rhs_dense)    */
+int orc_rk_batch_ex(const nngp_system *sys, int order, int mode, int n_slices, const double *t0,
+                    const double *t1, int64_t steps, const double *u0, double *uF, int nthreads, int dense) {
     int err = 0;
+    dense_ctx *dc = NULL;
+    if (dense) {
+        dc = dense_build(sys);
+        if (!dc) return -1;
+    }
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #pragma omp parallel for schedule(dynamic, 1) reduction(| : err)
 #endif
     for (int i = 0; i < n_slices; i++)
-        err |= orc_rk(sys, order, mode, t0[i], t1[i], steps, u0 + (size_t)i * sys->d,
-                      uF + (size_t)i * sys->d);
+        err |= rk_core(sys, dc, order, mode, t0[i], t1[i], steps, 0, steps,
+                       u0 + (size_t)i * sys->d, uF + (size_t)i * sys->d);
+    dense_free(dc);
     return err ? -1 : 0;
+}
+
+int orc_rk_batch(const nngp_system *sys, int order, int mode, int n_slices, const double *t0,
+                 const double *t1, int64_t steps, const double *u0, double *uF, int nthreads) {
+    return orc_rk_batch_ex(sys, order, mode, n_slices, t0, t1, steps, u0, uF, nthreads, 0);
 }
 
 /* ------------------------------------------------------------------------------------------ */
@@ -509,16 +684,57 @@ static double butterfly_sum(const double *v, int n) {
     return buf[0];
 }
 
+/* The reference's Cholesky is LAPACK dpotrf (jax.numpy.linalg.cholesky on CPU -> OpenBLAS; for
+ * n <= 32 its unblocked dpotf2_L):  ajj = a_jj - ddot(row j);  column j below the diagonal
+ * = (a_ij - A[j+1:, :j] @ L[j, :j]) via dgemv_n, then scaled by 1/ajj.  Its pass/fail bit on
+ * near-singular kernels (duplicated training rows: a jitter below psy*2^-53 is lost and K is
+ * psy*ones) steers Nelder-Mead -- a spurious pass yields a hugely negative -LML that wins the
+ * arg-min -- so the sums follow OpenBLAS's structure (x86_64 kernels; fma where its gcc build
+ * contracts), which agrees with numpy's LAPACK on pass/fail for ~99.6 % of duplicated-row kernels
+ * against ~89 % for subtracting the products one at a time:
+ *   diagonal  ddot over a strided row: two accumulators over groups of 4, t1 += fma(x0, x0, x2^2),
+ *             t2 += fma(x1, x1, x3^2), tail t1 = fma(x, x, t1); ddot = t1 + t2;
+ *   below     dgemv_n: rows in whole groups of 4 ("vector rows") add each 4-column block as
+ *             y -= fma(a3,x3, fma(a2,x2, fma(a1,x1, a0*x0))) and each leftover column as
+ *             y -= a*x; the last (n-j-1) & 3 rows ("tail rows") take y -= one fma chain over
+ *             all columns.                                                                  */
+static double potf2_dot(const double *x, int n) {
+    double t1 = 0.0, t2 = 0.0;
+    int i = 0;
+    for (; i + 4 <= n; i += 4) {
+        t1 = t1 + fma(x[i], x[i], x[i + 2] * x[i + 2]);
+        t2 = t2 + fma(x[i + 1], x[i + 1], x[i + 3] * x[i + 3]);
+    }
+    for (; i < n; i++) t1 = fma(x[i], x[i], t1);
+    return t1 + t2;
+}
+
+static double potf2_gemv_row(double y, const double *a, const double *x, int n, int vector_row) {
+    if (vector_row) {
+        int k = 0;
+        for (; k + 4 <= n; k += 4) {
+            double t = a[k] * x[k];
+            t = fma(a[k + 1], x[k + 1], t);
+            t = fma(a[k + 2], x[k + 2], t);
+            t = fma(a[k + 3], x[k + 3], t);
+            y = y - t;
+        }
+        for (; k < n; k++) y = y - a[k] * x[k];
+        return y;
+    }
+    double t = 0.0;
+    for (int k = 0; k < n; k++) t = fma(a[k], x[k], t);
+    return y - t;
+}
+
 /* Cholesky + solves for K = psy*exp(c*D2) + jit*I.  Returns 0 ok, 1 if potrf fails.
- * The reference's order belongs to LAPACK/OpenBLAS potrf + trsv inside jaxlib, so ONE order is
- * fixed here and in the HIP kernel: left-looking, row-oriented, every inner product a
- * sequential ascending sum of rounded products subtracted one at a time
- *     L_ij = (((K_ij - L_i0 L_j0) - L_i1 L_j1) - ...) * RN(1/L_jj),
- * forward z_i (k ascending), back alpha_i (k descending), each division the Markstein-
- * corrected x*RN(1/L_ii) (bitwise the IEEE quotient).  Of the orders tried against the
- * reference's own LML fixtures (tests/golden/lml.npz), this one agrees best on WHICH
- * near-singular kernels fail potrf (99.8 % of the duplicated-row grid, vs 99 % for a balanced
- * tree and 96 % for an FMA chain) -- the pass/fail bit that steers Nelder-Mead.               */
+ * The factorisation follows OpenBLAS dpotf2_L (potf2_dot / potf2_gemv_row above); on the
+ * reference's own LML fixtures (tests/golden/lml.npz) its pass/fail bit agrees on 99.8 % of the
+ * duplicated-row grid, and on 99.6 % of random duplicated / clustered kernels against numpy's
+ * LAPACK (89-97 % for subtracting the products one at a time, round 1's order, whose spurious
+ * passes on exactly duplicated neighbours -- FHN-PDE at its steady state -- derailed the run).
+ * The solves: forward z_i (k ascending), back alpha_i (k descending), successive subtraction,
+ * each division the Markstein-corrected x*RN(1/L_ii) (bitwise the IEEE quotient).            */
 static int gp_factor(int m, const double *D2, const double *y, double c, double psy, double jit,
                      double *L /*m*m*/, double *alpha) {
     /* build lower triangle (models.py:146-155, 88) */
@@ -530,18 +746,15 @@ static int gp_factor(int m, const double *D2, const double *y, double c, double 
         }
     double rinv_d[64];
     for (int j = 0; j < m; j++) {
-        double t = L[j * m + j];
-        for (int k = 0; k < j; k++) t = t - L[j * m + k] * L[j * m + k];
+        const double t = L[j * m + j] - potf2_dot(L + j * m, j);
         if (!(t > 0.0)) return 1;           /* ajj <= 0 or NaN: jax -> NaN -> +inf          */
         const double ljj = sqrt(t);
         const double rinv = 1.0 / ljj;
         L[j * m + j] = ljj;
         rinv_d[j] = rinv;
-        for (int i = j + 1; i < m; i++) {
-            double s = L[i * m + j];
-            for (int k = 0; k < j; k++) s = s - L[i * m + k] * L[j * m + k];
-            L[i * m + j] = s * rinv;
-        }
+        const int mm = m - 1 - j, m1 = mm & -4;
+        for (int i = j + 1; i < m; i++)
+            L[i * m + j] = potf2_gemv_row(L[i * m + j], L + i * m, L + j * m, j, i - j - 1 < m1) * rinv;
     }
     double z[64];
     for (int i = 0; i < m; i++) {

@@ -64,6 +64,7 @@ def lib():
         L.orc_rk.argtypes = [ctypes.POINTER(CSystem), i32, i32, dbl, dbl, i64, _dp, _dp]
         L.orc_rk_grid.argtypes = [ctypes.POINTER(CSystem), i32, i32, dbl, dbl, i64, i64, i64, _dp, _dp]
         L.orc_rk_batch.argtypes = [ctypes.POINTER(CSystem), i32, i32, i32, _dp, _dp, i64, _dp, _dp, i32]
+        L.orc_rk_batch_ex.argtypes = [ctypes.POINTER(CSystem), i32, i32, i32, _dp, _dp, i64, _dp, _dp, i32, i32]
         L.orc_nlml.argtypes = [i32, _dp, _dp, dbl, dbl, dbl]
         L.orc_nlml.restype = dbl
         L.orc_gp_mean_one.argtypes = [i32, _dp, _dp, _dp, dbl, dbl, dbl]
@@ -93,8 +94,12 @@ def _c(a):
 class System:
     """Oracle-side description of one vector field (+ optional '-11' wrapper)."""
 
-    def __init__(self, name, d=None, nx=0, normalized=True, param=(0.0, 0.0, 0.0, 0.0), mn=None, mx=None):
+    def __init__(self, name, d=None, nx=0, normalized=True, param=(0.0, 0.0, 0.0, 0.0), mn=None, mx=None,
+                 dense=False):
+        """dense=True (Burgers, FHN-PDE): rk_batch evaluates the field in the reference's dense
+        matrix formulation (systems.py:321-446) -- same results, the reference's cost."""
         self.name = name
+        self.dense = bool(dense)
         kind = SYS[name]
         if name in BOUNDS and d is None:
             d = len(BOUNDS[name][0])
@@ -152,8 +157,8 @@ class System:
         t1 = _c(t1)
         n = U0.shape[0]
         out = np.empty_like(U0)
-        rc = lib().orc_rk_batch(ctypes.byref(self.c), int(order), int(mode), n, _p(t0), _p(t1), int(steps),
-                                _p(U0), _p(out), int(nthreads))
+        rc = lib().orc_rk_batch_ex(ctypes.byref(self.c), int(order), int(mode), n, _p(t0), _p(t1), int(steps),
+                                   _p(U0), _p(out), int(nthreads), int(self.dense))
         assert rc == 0
         return out
 

@@ -2,13 +2,16 @@
 
 FETCH_SIZE / WRITE_SIZE are in KiB.  MI355X_MICROARCH.md: on gfx950 FETCH_SIZE reads 1/2 of the
 bytes of WIDE coalesced streaming reads; the fine kernel's reads are a few KiB of 8-byte loads,
-so the raw value is reported (no x2).  Per counter the MINIMUM over the launches is taken: the TCC
-counters are device-wide over a multi-second launch, and one pass has seen 685 KiB written during a
-launch whose own output is 3 KiB (another launch of the same pass: 3 KiB).
-Usage: python tools/pmc_traffic.py <fetch.csv> <write.csv> <out.json> [kernel-substring]
+so the raw value is reported (no x2).  Every launch is reported; the per-launch figure is the
+MEDIAN over the launches, with the minimum and maximum beside it.  The TCC counters are
+device-wide: over a multi-second launch they also count what else touches the device meanwhile
+(a pass once saw 685 KiB written during a launch whose own output is 3 KiB, the other launches
+of that pass 3 KiB), which the median does not hide and the max shows.
+Usage: python tools/pmc_traffic.py <fetch.csv> <write.csv> <out.json> [kernel-substring] [kernel_ms]
 """
 import csv
 import json
+import statistics
 import sys
 
 
@@ -23,13 +26,19 @@ def values(path, sub):
 def main():
     fetch, write, out = sys.argv[1:4]
     sub = sys.argv[4] if len(sys.argv) > 4 else 'rk_group_kernel'
+    kernel_ms = float(sys.argv[5]) if len(sys.argv) > 5 else None
     f, w = values(fetch, sub), values(write, sub)
-    res = {'kernel': sub, 'fetch_bytes_per_launch': min(f), 'write_bytes_per_launch': min(w),
+    res = {'kernel': sub, 'launches': len(f),
+           'fetch_bytes_median': statistics.median(f), 'fetch_bytes_min': min(f), 'fetch_bytes_max': max(f),
+           'write_bytes_median': statistics.median(w), 'write_bytes_min': min(w), 'write_bytes_max': max(w),
            'fetch_bytes_all_launches': f, 'write_bytes_all_launches': w}
-    res['bytes_per_launch'] = res['fetch_bytes_per_launch'] + res['write_bytes_per_launch']
-    res['launches'] = len(f)
+    res['bytes_per_launch'] = res['fetch_bytes_median'] + res['write_bytes_median']
+    res['bytes_per_launch_max'] = res['fetch_bytes_max'] + res['write_bytes_max']
+    if kernel_ms:
+        res['hbm_GBps'] = res['bytes_per_launch'] / (kernel_ms * 1e-3) / 1e9
+        res['hbm_frac_of_8TBps'] = res['hbm_GBps'] / 8000.0
     json.dump(res, open(out, 'w'), indent=1)
-    print(res)
+    print(json.dumps({k: v for k, v in res.items() if not k.endswith('all_launches')}))
 
 
 if __name__ == '__main__':
