@@ -401,17 +401,18 @@ def burgers_published_schedule(torch, g, sample_pages=2):
             'us_per_step': per_page / 39999 * 1e6}
 
 
-def ode_published_schedule(torch, g, ode, n, tspan, tab, eff, ref_s, ref_cores, sample_steps):
+def ode_published_schedule(torch, g, ode, n, tspan, tab, eff, ref_s, ref_cores, sample_steps, fma=False):
     """One ODE's published scalability schedule: time `sample_steps` of its `eff` effective fine
     steps per slice per iteration for all n slices (LINSPACE grids as the legacy RK_last, lane-group
     kernel) and scale to the iteration, next to the reference's F time per iteration on its
     cluster.  Each slice is one serial chain, so this compares per-step latency: a
-    CPU core per slice there, one GPU lane group per slice here."""
+    CPU core per slice there, one GPU lane group per slice here.  fma=True: the opt-in contracted
+    propagator (SolverRK(fma=True), tests/test_gpu_contract.py's 1e-12 tolerance)."""
     d = len(ode.get_init_cond())
     solver = g.SolverRK(ode.get_vector_field(), Ng=10, Nf=sample_steps, F=tab, G='RK1',
-                        step_mode='linspace', thresh=float('inf'))
+                        step_mode='linspace', thresh=float('inf'), fma=fma)
     small = g.SolverRK(ode.get_vector_field(), Ng=10, Nf=1000, F=tab, G='RK1', step_mode='linspace',
-                       thresh=float('inf'))
+                       thresh=float('inf'), fma=fma)
     t = np.linspace(tspan[0], tspan[1], n + 1)
     dev = lambda a: torch.tensor(a, dtype=torch.float64, device='cuda')
     rng = np.random.default_rng(0)
@@ -428,23 +429,24 @@ def ode_published_schedule(torch, g, ode, n, tspan, tab, eff, ref_s, ref_cores, 
     it = us * 1e-6 * eff
     return {'us_per_step': us, 'F_per_iteration_s': it, 'reference_F_per_iteration_s': ref_s,
             'reference_cores': ref_cores, 'speedup_vs_reference_F': ref_s / it, 'steps_per_slice': eff,
-            'sample': f'{sample_steps} of {eff:.3g} steps x {n} slices, {tab}, linspace'}
+            'sample': f'{sample_steps} of {eff:.3g} steps x {n} slices, {tab}, linspace',
+            'build': 'contracted (opt-in, 1e-12)' if fma else 'exact (bitwise the oracle)'}
 
 
-def tomlab_published_schedule(torch, g, sample_steps=1_000_000):
+def tomlab_published_schedule(torch, g, sample_steps=1_000_000, fma=False):
     """Thomas labyrinth N=256 (TomLab.py:83-101: Nf = Ng*ceil(1e9/Ng), RK4, RK_thresh = Nf/N/109):
     110 pages of the full per-slice count (new_lib.py:57-69) = 4.30e8 RK4 steps per
     slice per iteration; the reference's F per iteration on 282 cores was 156 s, 0.30-0.37 us/step."""
     return ode_published_schedule(torch, g, g.ThomasLabyrinth(normalization='-11'), 256, (0, 100), 'RK4',
-                                  4.30e8, 156.0, 282, sample_steps)
+                                  4.30e8, 156.0, 282, sample_steps, fma)
 
 
-def hopf_published_schedule(torch, g, sample_steps=500_000):
+def hopf_published_schedule(torch, g, sample_steps=500_000, fma=False):
     """Hopf N=128 (Hopf.py:60-69: Nf x 10^4, RK8, RK_thresh = Nf/N/25): 3.4e8 effective RK8 steps per
     slice per iteration (272 s / 0.80 us); the reference's F per iteration on 141
     cores was 272 s."""
     return ode_published_schedule(torch, g, g.Hopf(normalization='-11'), 128, (-20, 500), 'RK8',
-                                  3.4e8, 272.0, 141, sample_steps)
+                                  3.4e8, 272.0, 141, sample_steps, fma)
 
 
 def fhn_pde_fine_sweeps(torch, g):
@@ -698,6 +700,8 @@ def main():
         res['burgers_n128_published_schedule'] = burgers_published_schedule(torch, g)
         res['tomlab_n256_published_schedule'] = tomlab_published_schedule(torch, g)
         res['hopf_n128_published_schedule'] = hopf_published_schedule(torch, g)
+        res['tomlab_n256_published_schedule_contracted'] = tomlab_published_schedule(torch, g, fma=True)
+        res['hopf_n128_published_schedule_contracted'] = hopf_published_schedule(torch, g, fma=True)
         res['fhn_pde_n512_fine_sweep'] = fhn_pde_fine_sweeps(torch, g)
         res['cpu_baseline'] = cpu_baseline(args.steps_per_slice, args.slices_per_gpu)
         res['cpu_single_core'] = cpu_single_core()

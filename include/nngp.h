@@ -64,8 +64,13 @@ enum nngp_tableau { NNGP_RK1 = 1, NNGP_RK2 = 2, NNGP_RK4 = 4, NNGP_RK8 = 8 };
  *   FIXED:    h = (t1 - t0)/steps for every step          RK.run_get_last, RK.py:101-109
  *   LINSPACE: h_n = t[n+1] - t[n], t = np.linspace(t0, t1, steps+1)
  *             RK.run / legacy new_lib.RK (RK.py:91-99, new_lib.py:87-137) -- the convention
- *             of every published scalability run.                                            */
-enum nngp_step_mode { NNGP_STEP_FIXED = 0, NNGP_STEP_LINSPACE = 1 };
+ *             of every published scalability run.
+ * NNGP_STEP_CONTRACT (a flag OR-ed onto either mode; opt-in, not a reference behaviour): run the
+ *   propagator's second code object, compiled with a*b+c contracted to fma.  Fewer fp64
+ *   instructions per step (the fine sweep is instruction-issue-bound), results no longer bitwise
+ *   the reference's rounding order: per-slice end states agree to <= 1e-12 relative on the
+ *   test schedules (tests/test_gpu_contract.py).  Every other entry point ignores it.        */
+enum nngp_step_mode { NNGP_STEP_FIXED = 0, NNGP_STEP_LINSPACE = 1, NNGP_STEP_CONTRACT = 16 };
 
 /* One ODE/PDE right-hand side, optionally wrapped by the '-11' normalisation of
  * ODE.get_vector_field (systems.py:32-44, utils.py:14-33):

@@ -18,7 +18,7 @@ CSRC = os.path.join(HERE, 'csrc')
 SYS_LORENZ, SYS_HOPF, SYS_THOMAS_LABYRINTH, SYS_FHN_ODE, SYS_ROSSLER = 0, 1, 2, 3, 4
 SYS_BRUSSELATOR, SYS_DBL_PEND, SYS_BURGERS, SYS_FHN_PDE = 5, 6, 7, 8
 TABLEAU = {'RK1': 1, 'RK2': 2, 'RK4': 4, 'RK8': 8}
-STEP_FIXED, STEP_LINSPACE = 0, 1
+STEP_FIXED, STEP_LINSPACE, STEP_CONTRACT = 0, 1, 16
 
 EXPORTS = ['nngp_abi_version', 'nngp_last_error', 'nngp_device_count', 'nngp_rk_batch', 'nngp_rk_batch_grid',
            'nngp_rhs_batch', 'nngp_parareal_update', 'nngp_knn', 'nngp_nm_fit_batch',

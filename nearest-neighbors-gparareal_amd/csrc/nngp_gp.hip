@@ -1221,6 +1221,9 @@ static int wg_threads(int maxm) { return maxm > 32 ? 64 : 256; }
 // f<MAXM>() for the padded size of m
 template <typename F>
 static int with_maxm(int m, F &&f) {
+#ifdef NNGP_GP_ONLY_MAXM   // register/ISA experiments (tools): compile one padded size only
+    return f(std::integral_constant<int, NNGP_GP_ONLY_MAXM>{});
+#endif
     switch (maxm_for(m)) {
     case 8: return f(std::integral_constant<int, 8>{});
     case 16: return f(std::integral_constant<int, 16>{});

@@ -135,6 +135,14 @@ __device__ __forceinline__ void nn_sincos(double x, double &sn, double &cs) {
     // sign flips as sign-bit xors (a negation is exactly that, so this is the oracle's `-s_`)
     s_ = __longlong_as_double(__double_as_longlong(s_) ^ ((long long)(q & 2) << 62));
     c_ = __longlong_as_double(__double_as_longlong(c_) ^ ((long long)((q + 1) & 2) << 62));
+#ifdef NNGP_RK_FMA
+    // contracted propagator build: an inf/NaN argument already gives r = NaN (fma(-inf, PIO2_1,
+    // inf)), hence NaN polynomials; the exact build keeps the oracle's explicit select
+    (void)fin;
+    sn = s_;
+    cs = c_;
+    return;
+#endif
     const double nanv = x - x;                     // NaN for inf / NaN arguments
     sn = fin ? s_ : nanv;
     cs = fin ? c_ : nanv;

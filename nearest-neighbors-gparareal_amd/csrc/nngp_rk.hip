@@ -18,6 +18,12 @@
 // Numerics: compiled with -ffp-contract=off; every add/mul is rounded in the order of the
 // reference expression it restates (cited inline).  Zero tableau entries are skipped at compile
 // time, which is exact for finite stages (t + 0*k == t).
+//
+// This file is compiled TWICE (csrc/Makefile): the exact build above, and -- with NNGP_RK_FMA
+// defined and -ffp-contract=fast -- the opt-in contracted propagator (NNGP_STEP_CONTRACT,
+// include/nngp.h): the same kernels with every a*b+c fused, in the inline namespace `contracted`
+// so the two code objects' kernels never share a symbol.  Only the exact build exports the C-ABI;
+// the contracted one exports nngp_rk_dispatch_contracted, which nngp_rk_batch calls.
 
 #include <algorithm>
 
@@ -25,7 +31,14 @@
 #include "nngp_math.h"
 #include "tableau.h"
 
+#ifdef NNGP_RK_FMA
+#define NNGP_RK_VARIANT contracted
+#else
+#define NNGP_RK_VARIANT exact
+#endif
+
 namespace nngp {
+inline namespace NNGP_RK_VARIANT {
 
 // ---------------------------------------------------------------------------------------------
 // ODE right-hand sides (systems.py), one lane = one state
@@ -170,14 +183,27 @@ __device__ __forceinline__ double step_update(double u, const double *k, int c) 
 //           t[j] = j*gstep + t0 (gstep = (t1-t0)/gsteps), t[gsteps] = t1, h = t[j+1]-t[j]
 //           (RK.py:91-99, 121; new_lib.py:87-137).  j0 = 0, gsteps = steps is the per-slice grid;
 //           j0 > 0 walks one global grid (the legacy initial coarse sweep, new_lib.py:902-906).
-__device__ __forceinline__ double step_size(bool linspace, int64_t n, int64_t j0, int64_t gsteps,
-                                            double t0, double t1, double dt) {
-    if (!linspace) return dt;
-    const int64_t j = j0 + n;
-    const double tn = (double)j * dt + t0;
-    const double tn1 = (j + 1 == gsteps) ? t1 : (double)(j + 1) * dt + t0;
-    return tn1 - tn;
-}
+// The grid is walked with loop-carried state: jd = (double)j is bumped by an exact +1.0 (j < 2^53)
+// and t[j+1] of one step is t[j] of the next, so a step costs one grid point (add, mul, add, the
+// last-point select, sub) instead of two int64 -> double conversions and two grid points -- the
+// same values bit for bit, off the lane/group kernels' issue-bound step (TomLab RK4 267 -> 256
+// VALU per step).
+struct LinGrid {
+    double jd, tn;     // (double)j, t[j]
+    int64_t nlast;     // the step n with j + 1 == gsteps (its right end is t1 itself)
+    __device__ __forceinline__ void init(int64_t j0, int64_t gsteps, double t0, double dt) {
+        jd = (double)j0;
+        tn = jd * dt + t0;
+        nlast = gsteps - 1 - j0;
+    }
+    __device__ __forceinline__ double next(int64_t n, double t0, double t1, double dt) {
+        jd = jd + 1.0;
+        const double tn1 = (n == nlast) ? t1 : jd * dt + t0;
+        const double h = tn1 - tn;
+        tn = tn1;
+        return h;
+    }
+};
 
 template <int SYS, int ORDER, bool LINSPACE, bool NORM>
 __global__ void __launch_bounds__(64) rk_lane_kernel(LaneArgs args, int n_slices,
@@ -205,8 +231,10 @@ __global__ void __launch_bounds__(64) rk_lane_kernel(LaneArgs args, int n_slices
     const double T0 = t0[i], T1 = t1[i];
     const double dt = (T1 - T0) / (double)(LINSPACE ? gsteps : steps);
     const int64_t j0 = j0s ? j0s[i] : 0;
+    LinGrid grid;
+    if constexpr (LINSPACE) grid.init(j0, gsteps, T0, dt);
     for (int64_t n = 0; n < steps; n++) {
-        const double h = step_size(LINSPACE, n, j0, gsteps, T0, T1, dt);
+        const double h = LINSPACE ? grid.next(n, T0, T1, dt) : dt;
         // k_0 = h f(u); k_s = h f(u + sum_{j<s} a_sj k_j)     (RK.py:153-170)
 #pragma unroll
         for (int s = 0; s < S; s++) {
@@ -379,8 +407,10 @@ __global__ void __launch_bounds__(64) rk_group_kernel(LaneArgs args, int n_slice
     const double T0 = t0[i], T1 = t1[i];
     const double dt = (T1 - T0) / (double)(LINSPACE ? gsteps : steps);
     const int64_t j0 = j0s ? j0s[i] : 0;
+    LinGrid grid;
+    if constexpr (LINSPACE) grid.init(j0, gsteps, T0, dt);
     for (int64_t n = 0; n < steps; n++) {
-        const double h = step_size(LINSPACE, n, j0, gsteps, T0, T1, dt);
+        const double h = LINSPACE ? grid.next(n, T0, T1, dt) : dt;
 #pragma unroll
         for (int s = 0; s < S; s++) {
             const double tmp = stage_input<T, 1>(s, u, k, 0);
@@ -503,8 +533,10 @@ __global__ void __launch_bounds__(EPT == 1 ? 1024 : (EPT == 2 ? 512 : 256)) rk_f
     const double dt = (T1 - T0) / (double)(LINSPACE ? gsteps : steps);
     const int64_t j0 = j0s ? j0s[slice] : 0;
     int buf = 0;
+    LinGrid grid;
+    if constexpr (LINSPACE) grid.init(j0, gsteps, T0, dt);
     for (int64_t n = 0; n < steps; n++) {
-        const double h = step_size(LINSPACE, n, j0, gsteps, T0, T1, dt);
+        const double h = LINSPACE ? grid.next(n, T0, T1, dt) : dt;
 #pragma unroll
         for (int s = 0; s < S; s++) {
             double *V = smem + buf * d;
@@ -591,8 +623,10 @@ __global__ void __launch_bounds__(64) rk_burgers_wave_kernel(FieldArgs fa, int n
     const double T0 = t0[slice], T1 = t1[slice];
     const double dt = (T1 - T0) / (double)(LINSPACE ? gsteps : steps);
     const int64_t j0 = j0s ? j0s[slice] : 0;
+    LinGrid grid;
+    if constexpr (LINSPACE) grid.init(j0, gsteps, T0, dt);
     for (int64_t n = 0; n < steps; n++) {
-        const double h = step_size(LINSPACE, n, j0, gsteps, T0, T1, dt);
+        const double h = LINSPACE ? grid.next(n, T0, T1, dt) : dt;
 #pragma unroll
         for (int s = 0; s < S; s++) {
             double V[EPT];
@@ -898,7 +932,24 @@ static int launch_rhs_field(const nngp_system *sys, int n, const double *u, doub
     return NNGP_OK;
 }
 
+}  // namespace NNGP_RK_VARIANT
 }  // namespace nngp
+
+#ifdef NNGP_RK_FMA
+// the contracted code object's one entry (not part of include/nngp.h): same arguments as the exact
+// build's dispatch below
+extern "C" __attribute__((visibility("hidden"))) int nngp_rk_dispatch_contracted(
+    const nngp_system *sys, int tableau, int linspace, int n_slices, const double *t0, const double *t1,
+    int64_t steps, int64_t gsteps, const int64_t *j0, const double *u0, double *uF, void *stream) {
+    using namespace nngp;
+    hipStream_t st = (hipStream_t)stream;
+    if (linspace) return dispatch_tab<true>(sys, tableau, n_slices, t0, t1, steps, gsteps, j0, u0, uF, st);
+    return dispatch_tab<false>(sys, tableau, n_slices, t0, t1, steps, gsteps, j0, u0, uF, st);
+}
+#else
+extern "C" int nngp_rk_dispatch_contracted(const nngp_system *sys, int tableau, int linspace, int n_slices,
+                                           const double *t0, const double *t1, int64_t steps, int64_t gsteps,
+                                           const int64_t *j0, const double *u0, double *uF, void *stream);
 
 extern "C" int nngp_rhs_batch(const nngp_system *sys, int n, const double *u, double *out, void *stream) {
     using namespace nngp;
@@ -942,12 +993,14 @@ extern "C" int nngp_rk_batch(const nngp_system *sys, int tableau, int step_mode,
     if (n_slices == 0) return NNGP_OK;
     NNGP_REQUIRE(t0 && t1 && u0 && uF, "null array argument");
     hipStream_t st = (hipStream_t)stream;
-    if (step_mode == NNGP_STEP_FIXED)
+    const int mode = step_mode & ~NNGP_STEP_CONTRACT;
+    NNGP_REQUIRE(mode == NNGP_STEP_FIXED || mode == NNGP_STEP_LINSPACE, "unknown step_mode %d", step_mode);
+    if (step_mode & NNGP_STEP_CONTRACT)
+        return nngp_rk_dispatch_contracted(sys, tableau, mode == NNGP_STEP_LINSPACE, n_slices, t0, t1, steps,
+                                           steps, nullptr, u0, uF, stream);
+    if (mode == NNGP_STEP_FIXED)
         return dispatch_tab<false>(sys, tableau, n_slices, t0, t1, steps, steps, nullptr, u0, uF, st);
-    if (step_mode == NNGP_STEP_LINSPACE)
-        return dispatch_tab<true>(sys, tableau, n_slices, t0, t1, steps, steps, nullptr, u0, uF, st);
-    set_error("unknown step_mode %d", step_mode);
-    return NNGP_E_ARG;
+    return dispatch_tab<true>(sys, tableau, n_slices, t0, t1, steps, steps, nullptr, u0, uF, st);
 }
 
 extern "C" int nngp_rk_batch_grid(const nngp_system *sys, int tableau, int n_slices,
@@ -962,3 +1015,4 @@ extern "C" int nngp_rk_batch_grid(const nngp_system *sys, int tableau, int n_sli
     return dispatch_tab<true>(sys, tableau, n_slices, g0, g1, steps, gsteps, j0, u0, uF,
                               (hipStream_t)stream);
 }
+#endif  // NNGP_RK_FMA

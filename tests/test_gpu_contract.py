@@ -1,0 +1,93 @@
+"""The opt-in contracted propagator (SolverRK(fma=True) -> NNGP_STEP_CONTRACT, include/nngp.h): the
+same RK kernels compiled a second time with a*b+c fused to fma (csrc/Makefile, nngp_rk_contract.o).
+
+It is NOT bitwise the reference's rounding order, so it is held to a stated tolerance instead:
+  * per-slice end states within 1e-12 relative (max |a - b| / max(1, max |b|)) of the exact
+    build / the CPU oracle on every fixture system, tableau and step convention;
+  * the same converged iteration count K as the exact build on Lorenz Parareal (N=32), FHN-ODE
+    Parareal and nnGParareal (N=40), and Burgers nnGParareal (N=128, m=15) -- the configurations
+    whose K the exact build matches to the reference.
+The exact build stays the default (tests/test_gpu_kernels.py pins it bit for bit)."""
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import golden
+from systems_table import RK_KEYS, oracle_system, product_ode
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-12
+
+
+def _t(torch, a):
+    return torch.tensor(np.ascontiguousarray(a), dtype=torch.float64, device='cuda')
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+@pytest.mark.parametrize('key', RK_KEYS)
+@pytest.mark.parametrize('tab', ['RK4', 'RK8'])
+@pytest.mark.parametrize('mode', ['fixed', 'linspace'])
+def test_contracted_rk_within_tolerance_of_oracle(gpu, key, tab, mode):
+    import torch
+    R = golden('rk.npz')
+    k = f'{key}__{tab}'
+    u0 = R[k + '__u0']
+    t0, t1, steps = R[k + '__span']
+    ode = product_ode(gpu, key)
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=int(steps), Nf=int(steps), F=tab, G=tab, step_mode=mode, fma=True)
+    assert s.step_mode & 16
+    rng = np.random.default_rng(3)
+    U0 = u0[None, :] + 1e-3 * rng.standard_normal((5, len(u0)))
+    T0 = t0 + np.arange(5) * (t1 - t0)
+    T1 = T0 + (t1 - t0)
+    out = s.run_F_batch(_t(torch, T0), _t(torch, T1), _t(torch, U0)).cpu().numpy()
+    so = oracle_system(key)
+    m = O.STEP_FIXED if mode == 'fixed' else O.STEP_LINSPACE
+    ora = np.array([so.rk(int(tab[2:]), T0[i], T1[i], int(steps), U0[i], m) for i in range(5)])
+    for i in range(5):
+        assert _rel(out[i], ora[i]) <= TOL, (i, _rel(out[i], ora[i]))
+
+
+def test_contracted_build_is_a_different_code_object(gpu):
+    """The flag reaches the second code object: a long Hopf sweep differs in the last bits from the
+    exact build (and stays within the tolerance)."""
+    import torch
+    ode = gpu.Hopf(normalization='-11')
+    n, steps = 64, 20000
+    rng = np.random.default_rng(0)
+    U0 = _t(torch, rng.uniform(-0.5, 0.5, (n, 3)))
+    T0 = _t(torch, np.linspace(-20, 480, n))
+    T1 = T0 + 500 / n
+    ex = gpu.SolverRK(ode.get_vector_field(), Ng=4, Nf=steps, F='RK4', G='RK1').run_F_batch(T0, T1, U0)
+    fm = gpu.SolverRK(ode.get_vector_field(), Ng=4, Nf=steps, F='RK4', G='RK1', fma=True).run_F_batch(T0, T1, U0)
+    ex, fm = ex.cpu().numpy(), fm.cpu().numpy()
+    assert not np.array_equal(ex, fm)
+    assert max(_rel(fm[i], ex[i]) for i in range(n)) <= TOL
+
+
+def _k(gpu, ode, tspan, N, Ng, Nf, F, G, fma, **run):
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=Ng, Nf=Nf, F=F, G=G, fma=fma)
+    r = gpu.Parareal(ode, s, tspan, N, epsilon=5e-7, verbose=None).run(**run)
+    assert r['converged']
+    return r['k'], list(r['conv_int'])
+
+
+@pytest.mark.parametrize('case', ['lorenz_parareal', 'fhn_ode_parareal', 'fhn_ode_nngp', 'burgers_nngp'])
+def test_contracted_run_keeps_k(gpu, case):
+    if case == 'lorenz_parareal':
+        args = (gpu.Lorenz(normalization='-11'), [0, 18], 32, 6, 450, 'RK4', 'RK4')
+        run = dict(model='parareal')
+    elif case.startswith('fhn_ode'):   # test_gpu_parareal.test_fhn_ode_matches_reference's config
+        args = (gpu.FHN_ODE(normalization='-11'), [0, 40], 40, 4, 4000, 'RK4', 'RK2')
+        run = dict(model='parareal') if case.endswith('parareal') else dict(model='nngp', nn=15, seed=45)
+    else:
+        args = (gpu.Burgers(d_x=128, normalization='-11'), [0, 5], 128, 4, 2000, 'RK8', 'RK1')
+        run = dict(model='nngp', nn=15, seed=45)
+    ode, tspan, N, Ng, Nf, F, G = args
+    k_ex, c_ex = _k(gpu, ode, tspan, N, Ng, Nf, F, G, False, **run)
+    k_fm, c_fm = _k(gpu, ode, tspan, N, Ng, Nf, F, G, True, **run)
+    print(case, 'exact K', k_ex, 'contracted K', k_fm)
+    assert k_fm == k_ex

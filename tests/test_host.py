@@ -83,6 +83,20 @@ def test_solver_rejects_unknown_tableau():
         nngp_amd.SolverRK(lambda t, u: u, 6, 45, 'RK4', 'RK4')
 
 
+def test_contracted_propagator_is_opt_in(monkeypatch):
+    """SolverRK(fma=True) ORs NNGP_STEP_CONTRACT (include/nngp.h) onto either step convention; the
+    default is the exact build unless NNGP_RK_CONTRACT=1."""
+    import nngp_amd
+    f = nngp_amd.Lorenz().get_vector_field()
+    monkeypatch.delenv('NNGP_RK_CONTRACT', raising=False)
+    assert nngp_amd.SolverRK(f, 6, 45, 'RK4', 'RK4').step_mode == 0
+    assert nngp_amd.SolverRK(f, 6, 45, 'RK4', 'RK4', fma=True).step_mode == 16
+    assert nngp_amd.SolverRK(f, 6, 45, 'RK4', 'RK4', step_mode='linspace', fma=True).step_mode == 17
+    monkeypatch.setenv('NNGP_RK_CONTRACT', '1')
+    assert nngp_amd.SolverRK(f, 6, 45, 'RK4', 'RK4').fma
+    assert not nngp_amd.SolverRK(f, 6, 45, 'RK4', 'RK4', fma=False).fma
+
+
 def test_store_int_checkpoint_round_trip_without_gpu(tmp_path):
     """Checkpoints are npz + JSON (numpy safe loader, no pickle): arrays, scalars and the
     model's RNG state survive a round trip, and the restored RNG continues the same stream."""
