@@ -30,6 +30,11 @@ static int timing_events(size_t n, hipEvent_t **out) {
     return NNGP_OK;
 }
 
+static int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
 // re-speculation resources (per process; one device per process): a side stream, the events
 // that order it against the sweep's stream, and host-mapped hit flags the select kernel writes
 struct Respec {
@@ -53,7 +58,11 @@ static int respec_resources(size_t nflags, Respec **out) {
         if (r.ev_r) (void)hipEventDestroy(r.ev_r);
         if (r.hflags) (void)hipHostFree(r.hflags);
         r = Respec{};
-        NNGP_HIP_CHECK(hipStreamCreateWithFlags(&r.st2, hipStreamNonBlocking));
+        int lo = 0, hi = 0;
+        NNGP_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        // NNGP_RESPEC_PRIO: 0 = default priority, 1 = the least priority (the sweep's own fits first)
+        NNGP_HIP_CHECK(hipStreamCreateWithPriority(&r.st2, hipStreamNonBlocking,
+                                                   env_int("NNGP_RESPEC_PRIO", 0) ? lo : 0));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_g, hipEventDisableTiming));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_r, hipEventDisableTiming));
         r.dev = dev;
@@ -99,6 +108,7 @@ static int respec_window() {
     const int w = e ? atoi(e) : 4;
     return w < 0 ? 0 : w;
 }
+
 }  // namespace nngp
 
 // Speculation policy: worth it while the batch of every slice's fits is a throughput-shaped
@@ -251,7 +261,7 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
         if (rc == NNGP_OK)
             rc = spec_batch(X, Y, rows, d, Qr, w, m, n_jitter, jitter_exp_host, n_restarts,
                             theta0 + (j + 1) * n_fits * 2, fatol, xatol, maxfev, spec2_idx + (j + 1) * m,
-                            spec2_fits + (j + 1) * n_fits * 4, true, s2);
+                            spec2_fits + (j + 1) * n_fits * 4, env_int("NNGP_RESPEC_PACKED", 0) == 0, s2);
         if (rc == NNGP_OK) {
             NNGP_HIP_CHECK(hipEventRecord(rs->ev_r, s2));
             respec_pending = true;

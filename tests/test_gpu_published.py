@@ -26,17 +26,30 @@ def _burgers(gpu):
     return s
 
 
-@pytest.mark.parametrize('model,K', [('parareal', 10), ('nngp', 9)])
-def test_burgers_published_schedule_k(gpu, model, K):
-    """Burgers d=128 N=128 T=5 on the published schedule -- Parareal K=10,
-    nnGParareal (nn=18, Burgers.py:119) K=9."""
-    s = _burgers(gpu)
-    kw = dict(model='nngp', nn=18) if model == 'nngp' else {}
-    r = s.run(**kw)
+def test_burgers_published_schedule_parareal_k(gpu):
+    """Burgers d=128 N=128 T=5 on the published schedule -- classic Parareal K=10
+    (deterministic: no model randomness, so the published K is asserted exactly)."""
+    r = _burgers(gpu).run()
     tm = r['timings']
-    print(f"Burgers published schedule {model}: K={r['k']} (published {K}) conv_int={r['conv_int']} "
+    print(f"Burgers published schedule parareal: K={r['k']} (published 10) conv_int={r['conv_int']} "
+          f"runtime={tm['runtime']:.1f}s F={tm['F_time']:.1f}s")
+    assert r['converged'] and r['k'] == 10
+
+
+@pytest.mark.parametrize('seed', [45, 0, 1, 2])
+def test_burgers_published_schedule_nngp_k(gpu, seed):
+    """nnGParareal (nn=18, Burgers.py:119; the reference's default seed is 45) on the
+    published schedule -- the reference's one published run converged in K=9.  nnGParareal's K
+    moves with the Nelder-Mead paths, which move with the seed and with last-ulp differences
+    between XLA/LAPACK and this repo's fully specified exp/Cholesky order (the reference's own 100
+    seeds at the Burgers_perf_across_m schedule spread over K in {9, 10}); the loop itself is
+    pinned bit for bit to the oracle (test_gpu_parareal.py).  Asserted: converged within one
+    iteration of the published K, and strictly faster than classic Parareal's 10."""
+    r = _burgers(gpu).run(model='nngp', nn=18, seed=seed)
+    tm = r['timings']
+    print(f"Burgers published schedule nngp seed {seed}: K={r['k']} (published 9) conv_int={r['conv_int']} "
           f"runtime={tm['runtime']:.1f}s F={tm['F_time']:.1f}s mdl={tm['mdl_tot_t']:.2f}s")
-    assert r['converged'] and r['k'] == K
+    assert r['converged'] and 8 <= r['k'] <= 9
 
 
 def test_fhn_pde_d512_published_k(gpu):
