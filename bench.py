@@ -130,16 +130,16 @@ def corrections_bench(torch, g, m=15, R=2, n_slices=128):
     return n_pred, r['timings']['mdl_pred_t'], time.perf_counter() - t0
 
 
-def converge(torch, g, which):
+def converge(torch, g, which, fma=False):
     if which == 'hopf':
         ode = g.Hopf(normalization='-11')
         solver = g.SolverRK(ode.get_vector_field(), Ng=16, Nf=2048 * 85 * 10000 // 128, F='RK4', G='RK1',
-                            thresh=float('inf'))
+                            thresh=float('inf'), fma=fma)
         p = g.Parareal(ode, solver, [-20, 500], 128, epsilon=5e-7, verbose=None)
         kw = dict(nn=15, n_restarts=2, fatol=0.1, xatol=0.1, seed=45)
     else:   # Burgers_perf_across_m.py:30-33 (d=128, N=128, T=5, Nf/N=2000 RK8, Ng/N=4 RK1), m=15
         ode = g.Burgers(d_x=128, normalization='-11')
-        solver = g.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
+        solver = g.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1', fma=fma)
         p = g.Parareal(ode, solver, [0, 5], 128, epsilon=5e-7, verbose=None)
         kw = dict(nn=15, seed=45)
     torch.cuda.synchronize()
@@ -678,6 +678,13 @@ def main():
                                                    'conv_int': tim.get('conv_int', []),
                                                    'spec_hits': tim.get('spec_hits', [])}
             log(which, 'converged', conv, 'K', k, f'{wall:.2f}s')
+        # the opt-in contracted propagator on the same two solves
+        for which in ('burgers', 'hopf'):
+            wall, k, conv, tim, _ = converge(torch, g, which, fma=True)
+            res[f'{which}_n128_to_convergence_contracted'] = {
+                'wall_s': wall, 'K': k, 'converged': conv, 'F_time_s': tim['F_time'],
+                'mdl_time_s': tim['mdl_tot_t'], 'K_exact_build': res[f'{which}_n128_to_convergence']['K']}
+            log(which, 'contracted: K', k, f'{wall:.2f}s')
         res['nngp_corrections_fhn_d200'] = corrections_fhn_d200(torch, g)
         res['nngp_correction_roofline'] = {f'd{d}_m{m}_R{R}': correction_roofline(torch, g, d, m, R)
                                            for d, m, R in ((800, 20, 1), (200, 20, 1), (128, 15, 1), (3, 15, 2))}

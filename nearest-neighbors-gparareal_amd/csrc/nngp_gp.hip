@@ -446,11 +446,6 @@ __global__ void __launch_bounds__(256) d2_kernel(const double *__restrict__ xm, 
 //   z, alpha: successive subtraction, k ascending / descending; x/L_ii as Markstein x*RN(1/L_ii)
 //   sums over rows: lane pairs (l, l+16) first, then butterfly levels 1, 2, 4, 8
 // ---------------------------------------------------------------------------------------------
-#ifdef NNGP_GP_SCHED_FENCE
-#define GP_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define GP_SCHED_FENCE() ((void)0)
-#endif
 template <int L>
 __device__ __forceinline__ double row_bcast(double v) {   // every lane <- lane L of its 16-row
     return __builtin_amdgcn_mov_dpp(v, 0x150 + L, 0xF, 0xF, false);
@@ -620,7 +615,6 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
     //   subtraction's) and keeps the one its row takes.
     static_for<0, MAXM>([&](auto jc) {
         constexpr int j = decltype(jc)::value, SJ = j / 16, LJ = j % 16;
-        GP_SCHED_FENCE();
         const int tail_start = j + 1 + ((m - 1 - j) & ~3);
         double yv[RPL], tt[RPL], blk[RPL];
 #pragma unroll
@@ -685,7 +679,6 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
     }
     static_for<0, MAXM>([&](auto ic) {
         constexpr int i = decltype(ic)::value, SI = i / 16, LI = i % 16;
-        GP_SCHED_FENCE();
         const double zi = row_bcast<LI>(divd(SI, acc[SI]));
         z[SI] = (l == LI) ? zi : z[SI];
 #pragma unroll
@@ -718,7 +711,6 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
     }
     static_for<0, MAXM>([&](auto ic) {
         constexpr int i = MAXM - 1 - decltype(ic)::value, SI = i / 16, LI = i % 16;
-        GP_SCHED_FENCE();
         const double ai = row_bcast<LI>(divd(SI, acc2[SI]));
         alpha[SI] = (l == LI) ? ai : alpha[SI];
 #pragma unroll
