@@ -34,7 +34,8 @@ namespace nngp {
 
 static constexpr int GPB = GPF_PANEL;                // panel width
 static constexpr double GPF_LOG_2PI = 1.8378770664093453;   // np.log(2*np.pi)
-static constexpr int GPF_MAX_ROWS = 7936;            // alpha_kernel keeps the vector in LDS (<= 62 KB)
+static constexpr int GPF_LDS_ROWS = 7936;            // alpha_kernel keeps the vector in LDS (<= 62 KB) up to here,
+                                                     // beyond it in its own output row (no row limit)
 
 __device__ __forceinline__ void wave_sync_lds() {   // order one wave's LDS writes before its reads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -279,7 +280,9 @@ __global__ void __launch_bounds__(256) gpf_lml_kernel(const double *__restrict__
 
 // alpha = L^-T z (the second solve_triangular of _fit_gp_np / _predict's weights), 32-row blocks
 // bottom-up: the block's L staged in LDS, wave 0 solves it in registers (alpha_j read from lane
-// j), the workgroup updates the rows above
+// j), the workgroup updates the rows above.  The working vector lives in LDS up to GPF_LDS_ROWS
+// rows and in the point's alpha_out row beyond (the same arithmetic; the rows grow by N+1-I per
+// Parareal iteration, so long GParareal runs pass the LDS size -- the reference has no limit)
 __global__ void __launch_bounds__(256) gpf_alpha_kernel(const double *__restrict__ A, int n,
                                                          const int32_t *__restrict__ fail,
                                                          double *__restrict__ alpha_out) {
@@ -288,7 +291,8 @@ __global__ void __launch_bounds__(256) gpf_alpha_kernel(const double *__restrict
     const int ld = n + 1;
     const double *Ab = A + (size_t)b * ld * ld;
     const int tid = threadIdx.x, lane = tid & 63;
-    extern __shared__ double r[];   // [n]
+    extern __shared__ double r_lds[];   // [n] when n <= GPF_LDS_ROWS
+    double *r = (n <= GPF_LDS_ROWS) ? r_lds : alpha_out + (size_t)b * n;
     __shared__ double Lb[GPB][GPB + 1];
     for (int i = tid; i < n; i += 256) r[i] = Ab[(size_t)n * ld + i];
     __syncthreads();
@@ -320,7 +324,8 @@ __global__ void __launch_bounds__(256) gpf_alpha_kernel(const double *__restrict
         }
         __syncthreads();
     }
-    for (int i = tid; i < n; i += 256) alpha_out[(size_t)b * n + i] = r[i];
+    if (n <= GPF_LDS_ROWS)
+        for (int i = tid; i < n; i += 256) alpha_out[(size_t)b * n + i] = r[i];
 }
 
 // posterior mean of every coordinate j at one query q (models.py:456-462 -> _predict :441-453):
@@ -375,7 +380,8 @@ static int gpf_eval(const double *D2, int n, const double *Y, int d, const GPPoi
     hipLaunchKernelGGL(gpf_lml_kernel, dim3(nb), dim3(256), 0, st, A, n, fail, fval);
     NNGP_LAUNCH_CHECK();
     if (alpha_out) {
-        hipLaunchKernelGGL(gpf_alpha_kernel, dim3(nb), dim3(256), sizeof(double) * n, st, A, n, fail, alpha_out);
+        hipLaunchKernelGGL(gpf_alpha_kernel, dim3(nb), dim3(256), n <= GPF_LDS_ROWS ? sizeof(double) * n : 0, st, A,
+                           n, fail, alpha_out);
         NNGP_LAUNCH_CHECK();
     }
     return NNGP_OK;
@@ -414,8 +420,7 @@ static int gpf_workspace(int n, int nb, GPFWork &w) {
 }
 
 static int gpf_check(int64_t rows, int d, int n_fit) {
-    NNGP_REQUIRE(rows >= 1 && rows <= GPF_MAX_ROWS, "full GP needs 1 <= rows <= %d (got %lld)", GPF_MAX_ROWS,
-                 (long long)rows);
+    NNGP_REQUIRE(rows >= 1 && rows <= (int64_t)1 << 30, "full GP needs 1 <= rows (got %lld)", (long long)rows);
     NNGP_REQUIRE(d >= 1 && n_fit >= 1, "bad d / fit count");
     return NNGP_OK;
 }

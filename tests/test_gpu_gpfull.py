@@ -88,6 +88,25 @@ def test_gpfull_lml_and_weights_vs_oracle(gpu, n):
             assert res <= 1e-12 * (np.abs(K).sum(1).max() * np.abs(al[i]).max() + np.abs(yy).max()), (n, i, res)
 
 
+def test_gpfull_weights_beyond_the_lds_vector(gpu):
+    """More training rows than the alpha solve's LDS vector (7 936): the solve keeps the vector in
+    the point's own output row instead -- no row limit, as in the reference's GPjax_p (the rows
+    grow by N+1-I per iteration).  A well-conditioned kernel, so the -LML is held to 1e-9 relative
+    of the oracle and the weights to a backward-stable residual."""
+    import torch
+    n = 8200
+    rng = np.random.default_rng(8200)
+    x = rng.uniform(-1, 1, (n, 2))
+    y = np.sin(2 * x) + 0.01 * rng.standard_normal((n, 2))
+    theta, jit = (0.3, 0.8), -4.0
+    fv, al = _lml(gpu, torch, x, y, [1], [jit], [theta], alpha=True)
+    ref = GF.gp_nlml(x, y[:, 1], np.array(theta), jit)
+    assert _close(fv[0], ref, 1e-9), (fv[0], ref)
+    K = GF.gp_kernel(x, x, np.array(theta)) + np.eye(n) * 10 ** jit
+    res = np.abs(K @ al[0] - y[:, 1]).max()
+    assert res <= 1e-12 * (np.abs(K).sum(1).max() * np.abs(al[0]).max() + np.abs(y[:, 1]).max()), res
+
+
 def test_gpfull_fit_matches_reference_fits(gpu):
     """nngp_gpfull_fit on the reference's recorded training fan-outs (models.py:404-407): every
     coordinate's selected optimum (models.py:388-395) matches the reference's."""
