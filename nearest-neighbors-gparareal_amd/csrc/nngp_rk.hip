@@ -580,6 +580,86 @@ __global__ void __launch_bounds__(EPT == 1 ? 1024 : (EPT == 2 ? 512 : 256)) rk_f
 }
 
 // ---------------------------------------------------------------------------------------------
+// FHN-PDE with one thread per grid point: thread p owns u[p] and v[p] (elements p and half + p)
+// with all their stage values.  The reaction terms couple u and v at the SAME point and the
+// Laplacian's centre is the point itself, so a stage reads from LDS only the two 5-point
+// Laplacians (the own and partner values come from registers): 1 write + 10 reads per point
+// instead of the element-per-thread kernel's 2 writes + 14 reads.  Same expressions, same order
+// (systems.py:365-366) -- bitwise rk_field_kernel<FHN_PDE>.  d = 2 nx^2 <= 2048.
+// ---------------------------------------------------------------------------------------------
+template <int ORDER, bool LINSPACE, bool NORM>
+__global__ void __launch_bounds__(1024) rk_fhn_pair_kernel(FieldArgs fa, int n_slices,
+                                                           const double *__restrict__ t0,
+                                                           const double *__restrict__ t1, int64_t steps,
+                                                           int64_t gsteps, const int64_t *__restrict__ j0s,
+                                                           const double *__restrict__ u0,
+                                                           double *__restrict__ uF) {
+    using T = Tableau<ORDER>;
+    constexpr int S = T::S;
+    extern __shared__ __attribute__((aligned(16))) double smem[];   // [2][d]
+    const int slice = blockIdx.x;
+    const int p = threadIdx.x;
+    const int d = fa.d, half = d / 2;
+    const bool ok = p < half;
+    double u[2], k[S * 2], mn[2], w[2], sc[2];
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const int e = p + r * half;
+        u[r] = ok ? u0[(size_t)slice * d + e] : 0.0;
+        if (NORM && ok) {
+            mn[r] = fa.norm[e];
+            w[r] = 0.5 * fa.norm[d + e];   // (mx-mn)/2, see lane_rhs
+            sc[r] = fa.norm[2 * d + e];
+        } else {
+            mn[r] = 0.0; w[r] = 1.0; sc[r] = 1.0;
+        }
+    }
+    const Nbr5 nb = fhn_neighbours(fa.nx, ok ? p : 0);   // the same stencil for u and v
+    const double T0 = t0[slice], T1 = t1[slice];
+    const double dt = (T1 - T0) / (double)(LINSPACE ? gsteps : steps);
+    const int64_t j0 = j0s ? j0s[slice] : 0;
+    int buf = 0;
+    LinGrid grid;
+    if constexpr (LINSPACE) grid.init(j0, gsteps, T0, dt);
+    for (int64_t n = 0; n < steps; n++) {
+        const double h = LINSPACE ? grid.next(n, T0, T1, dt) : dt;
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+            double *V = smem + buf * d;
+            double xw[2];
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+                const double x = stage_input<T, 2>(s, u[r], k, r);
+                xw[r] = NORM ? (x + 1) * w[r] + mn[r] : x;
+                if (ok) V[p + r * half] = xw[r];
+            }
+            __syncthreads();
+            double fu = 0.0, fv = 0.0;
+            if (ok) {   // systems.py:365-366, as rk_field_kernel with V[e] / V[half+e] / V[e-half] in registers
+                const double lu = fhn_lap(V, nb, fa.a_off, fa.a_diag);
+                const double u1 = xw[0], u1c = u1 * (u1 * u1);
+                fu = (((lu + u1) - u1c) - xw[1]) + -5E-3 * 1.0;
+                const double lv = fhn_lap(V + half, nb, fa.b_off, fa.b_diag);
+                fv = (1 / 0.1) * ((lv + xw[0]) - xw[1]);
+                if (NORM) {
+                    fu = fu * sc[0];
+                    fv = fv * sc[1];
+                }
+            }
+            k[s * 2 + 0] = h * fu;
+            k[s * 2 + 1] = h * fv;
+            buf ^= 1;
+        }
+#pragma unroll
+        for (int r = 0; r < 2; r++) u[r] = step_update<T, 2>(u[r], k, r);   // RK.py:170
+    }
+    if (ok) {
+        uF[(size_t)slice * d + p] = u[0];
+        uF[(size_t)slice * d + half + p] = u[1];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Burgers with d = 64*EPT: ONE WAVE per slice, no LDS, no barriers.
 // Lane l owns the contiguous elements l*EPT .. l*EPT+EPT-1; the periodic stencil's outer
 // neighbours come from lanes l-1 / l+1 by `wave_ror:1` / `wave_rol:1` DPP moves, which wrap around
@@ -859,6 +939,25 @@ static int launch_field(const nngp_system *sys, int n, const double *t0, const d
         if (e == 2) return launch_burgers_wave<ORDER, LIN, 2>(fa, n, t0, t1, steps, gsteps, j0, u0, uF, st);
         if (e == 3) return launch_burgers_wave<ORDER, LIN, 3>(fa, n, t0, t1, steps, gsteps, j0, u0, uF, st);
         return launch_burgers_wave<ORDER, LIN, 4>(fa, n, t0, t1, steps, gsteps, j0, u0, uF, st);
+    }
+    // FHN-PDE from 16x16 grid points: one thread per point (u and v of the point) unless
+    // NNGP_FHN_PAIR=0 or a thread count is forced.  Measured (tools/contract_probe.py): d = 800 at
+    // 512 slices 7.50 -> 6.75 us/step, at 64 slices unchanged; d = 200 (100 points: 28 of 128
+    // lanes idle) 3.65 -> 4.25, so small grids keep the element kernel's 64 threads x 4
+    if (SYS == NNGP_SYS_FHN_PDE && sys->d / 2 >= 256 && sys->d / 2 <= 1024 && !getenv("NNGP_RK_THREADS")) {
+        const char *pe = getenv("NNGP_FHN_PAIR");
+        if (!pe || atoi(pe) != 0) {
+            const int bt = ((sys->d / 2 + 63) / 64) * 64;
+            const size_t lds = sizeof(double) * 2 * (size_t)sys->d;
+            if (fa.normalized)
+                hipLaunchKernelGGL((rk_fhn_pair_kernel<ORDER, LIN, true>), dim3(n), dim3(bt), lds, st, fa, n, t0, t1,
+                                   steps, gsteps, j0, u0, uF);
+            else
+                hipLaunchKernelGGL((rk_fhn_pair_kernel<ORDER, LIN, false>), dim3(n), dim3(bt), lds, st, fa, n, t0, t1,
+                                   steps, gsteps, j0, u0, uF);
+            NNGP_LAUNCH_CHECK();
+            return NNGP_OK;
+        }
     }
     const int bt = pick_threads(sys->d, n);
     const int ept = (sys->d + bt - 1) / bt;

@@ -111,6 +111,34 @@ def test_field_kernel_thread_overrides(gpu, nx, monkeypatch):
                 s.run_F_batch(T0, T1, U0)
 
 
+@pytest.mark.parametrize('nx,norm,mode', [(4, None, 'fixed'), (10, '-11', 'linspace'), (16, None, 'fixed'),
+                                          (20, None, 'linspace'), (20, '-11', 'fixed'), (32, None, 'fixed')])
+def test_fhn_point_pair_kernel_equals_element_kernel(gpu, nx, norm, mode, monkeypatch):
+    """FHN-PDE's point-pair field kernel (one thread per grid point: u and v of the point, the
+    reaction terms' own/partner values from registers; the default from 16x16 points) is bitwise
+    the element-per-thread kernel (NNGP_FHN_PAIR=0) and the oracle, fixed and linspace grids, RK4
+    and RK8, up to d = 2048 (below 16x16 both runs take the element kernel)."""
+    import torch
+    ode = gpu.FHN_PDE(d_x=nx, normalization=norm) if norm else gpu.FHN_PDE(d_x=nx)
+    d = 2 * nx * nx
+    rng = np.random.default_rng(nx)
+    n = 5
+    U0 = np.clip(ode.get_init_cond()[None, :] + 0.01 * rng.standard_normal((n, d)), -1, 1)
+    T0 = np.arange(n) * 0.05
+    T1 = T0 + 0.05   # inside the explicit stability limit of the finest grid's diffusion
+    for tab in ('RK4', 'RK8'):
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=1, Nf=12, F=tab, G='RK1', step_mode=mode)
+        monkeypatch.delenv('NNGP_FHN_PAIR', raising=False)
+        pair = s.run_F_batch(_t(torch, T0), _t(torch, T1), _t(torch, U0)).cpu().numpy()
+        monkeypatch.setenv('NNGP_FHN_PAIR', '0')
+        elem = s.run_F_batch(_t(torch, T0), _t(torch, T1), _t(torch, U0)).cpu().numpy()
+        assert np.all(np.isfinite(pair)) and np.array_equal(pair, elem), (nx, tab)
+        so = O.System('fhn_pde', nx=nx, mn=-1, mx=1) if norm else O.System('fhn_pde', nx=nx, normalized=False)
+        m = O.STEP_FIXED if mode == 'fixed' else O.STEP_LINSPACE
+        ora = np.array([so.rk(int(tab[2:]), T0[i], T1[i], 12, U0[i], m) for i in range(n)])
+        assert np.array_equal(pair, ora), (nx, tab)
+
+
 def test_rk_batch_uF_may_alias_u0(gpu):
     import torch
     ode = gpu.Burgers(d_x=128, normalization='-11')
