@@ -613,8 +613,15 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
     //           leftover columns y -= a*x; "tail rows" (the last (m-1-j) & 3): y -= one fma chain.
     //   Each lane evaluates both row forms (their operation counts add up to the old successive
     //   subtraction's) and keeps the one its row takes.
+    // Once EVERY row of the wave has a failed pivot (each row is a fit, or a candidate of one
+    // fit), the -LML of all of them is +inf whatever follows: the remaining columns, both solves
+    // and the L write-back are skipped (a scalar branch per column).  Fits that wander where the
+    // kernel is singular for their jitter -- near-duplicate neighbours, FHN-PDE at its steady
+    // state -- evaluate +inf until maxfev (~8 % of a d = 800 correction's fits, the whole tail).
+    bool dead = false;   // wave-uniform
     static_for<0, MAXM>([&](auto jc) {
         constexpr int j = decltype(jc)::value, SJ = j / 16, LJ = j % 16;
+        if (dead) return;
         const int tail_start = j + 1 + ((m - 1 - j) & ~3);
         double yv[RPL], tt[RPL], blk[RPL];
 #pragma unroll
@@ -656,6 +663,7 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
         t[SJ] = (l == LJ) ? a[SJ][j] - (d1 + d2) : t[SJ];
         const double piv = row_bcast<LJ>(t[SJ]);
         fail = fail || !(piv > 0.0);
+        dead = __all(fail);
         const double ljj = sqrt(piv);
         const double ri = 1.0 / ljj;
         diag[SJ] = (l == LJ) ? ljj : diag[SJ];
@@ -664,6 +672,11 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
         for (int s = 0; s < RPL; s++)
             if (16 * (s + 1) > j) a[s][j] = (l + 16 * s == j) ? ljj : t[s] * ri;
     });
+    if (dead) {
+#pragma unroll
+        for (int s = 0; s < RPL; s++) alpha[s] = 0.0;
+        return false;
+    }
     // x / L_ii for this lane's row of set s: Markstein-corrected x * RN(1/L_ii) (= IEEE x/L_ii)
     auto divd = [&](int s, double x) {
         const double q = x * rinv[s];
