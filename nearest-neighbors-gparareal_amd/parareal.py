@@ -117,13 +117,21 @@ def fine_sweep_sharded(propagate, t, U, UF, I, N, group=None):
     if hi > lo:
         propagate(t[lo:hi], t[lo + 1:hi + 1], U[lo:hi].contiguous(), send[:hi - lo])
     if dist.get_backend(group) == 'gloo':
-        parts = [torch.empty_like(send) for _ in range(world)]
-        dist.all_gather(parts, send, group=group)
-        gathered = torch.cat(parts)
+        gathered = _gloo_all_gather(send, group, world)
     else:
         gathered = torch.empty((world * chunk, n), dtype=U.dtype, device=U.device)
         dist.all_gather_into_tensor(gathered, send, group=group)
     UF[I + 1:N + 1] = gathered[:N - I]
+
+
+def _gloo_all_gather(send, group, world):
+    """gloo's list all-gather; device tensors are staged through host memory (several ranks
+    sharing one GPU, where RCCL refuses duplicate devices -- the multi-rank GPU tests)."""
+    import torch
+    host = send.detach().cpu()
+    parts = [torch.empty_like(host) for _ in range(world)]
+    torch.distributed.all_gather(parts, host, group=group)
+    return torch.cat(parts).to(send.device)
 
 
 def _all_gather_flat(send, group, world):
@@ -132,9 +140,7 @@ def _all_gather_flat(send, group, world):
     import torch
     dist = torch.distributed
     if dist.get_backend(group) == 'gloo':
-        parts = [torch.empty_like(send) for _ in range(world)]
-        dist.all_gather(parts, send, group=group)
-        return torch.cat(parts)
+        return _gloo_all_gather(send, group, world)
     out = torch.empty((world * send.shape[0],) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
     dist.all_gather_into_tensor(out, send, group=group)
     return out

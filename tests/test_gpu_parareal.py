@@ -104,6 +104,26 @@ def test_tomlab_nngp_bitwise_equals_oracle_loop(gpu):
     assert np.array_equal(np.nan_to_num(r['u'], nan=7.0), np.nan_to_num(o['u'], nan=7.0))
 
 
+def test_tomlab_n256_nngp_bitwise_equals_oracle_loop(gpu):
+    """BASELINE configs[3]'s size: ThomasLabyrinth N=256 on configs.py's schedule for N=256
+    (configs.py:50-57: T=100, Ng/N=10 RK1, Nf/N=3 910 RK4) with TomLab.py's nnGP settings (m=18,
+    fatol=xatol=1e-3), three iterations: every iterate bitwise the oracle's loop."""
+    from nngp_amd.configs import Config
+    ode = gpu.ThomasLabyrinth(normalization='-11')
+    cfg = Config(gpu.ThomasLabyrinth(normalization='-11'), N=256).get()
+    Ng, Nf = cfg['Ng'], cfg['Nf']
+    assert (Ng, Nf, cfg['tspan']) == (10, 3910, [0, 100])
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=Ng, Nf=Nf, F='RK4', G='RK1')
+    p = gpu.Parareal(ode, s, [0, 100], 256, epsilon=5e-7, verbose=None)
+    kw = dict(nn=18, n_restarts=1, fatol=1e-3, xatol=1e-3, seed=45, early_stop=3)
+    r = p.run(model='nngp', **kw)
+    so = O.System('tomlab')
+    o = O.parareal(so, [0, 100], 256, Ng, Nf, 'RK1', 'RK4', model='nngp', nn=18, seed=45, fatol=1e-3,
+                   xatol=1e-3, u0=so.fit([4.6722764, 5.2437205e-10, -6.4444208e-10]), early_stop=3)
+    assert r['k'] == o['k'] and r['conv_int'] == o['conv_int']
+    assert np.array_equal(np.nan_to_num(r['u'], nan=7.0), np.nan_to_num(o['u'], nan=7.0))
+
+
 def test_burgers_n128_first_iteration_bitwise_equals_oracle(gpu):
     """BASELINE configs[2] (Burgers d=128, N=128, RK8 2000/RK1 4 per slice, m=15): the first
     iteration -- 128 fine solves and 127 sequential corrections of 1 152 fits each -- is bitwise
