@@ -819,6 +819,10 @@ struct NMArgs {
     // reaches park_cap (its Nelder-Mead state, pending request included, in park[f], f appended to
     // park_list); the speculative kernel then resumes the parked fits (resume != 0), a wave each
     int park_cap, resume;
+    // unfused fits in product order (coord null): rows take fits jitter-major (slot s -> fit
+    // (s % d) * nfc + s / d), so a wave's rows share a jitter (and, for R = 1, differ in the
+    // coordinate only); the kernel matrix K depends on (theta, jitter), not on the coordinate
+    int jmajor;
     NM *park;
     int32_t *park_list, *park_count;
 };
@@ -884,6 +888,7 @@ __global__ void __launch_bounds__(NMBound<MAXM>::T) nm_fit_kernel(NMArgs a) {
         } else {
             f = blockIdx.x * ngroups + g;
             valid = f < a.n_fits;
+            if (valid && a.jmajor && !a.coord) f = (f % a.d) * nfc + f / a.d;
         }
     }
     double y[RPL];
@@ -957,6 +962,7 @@ __global__ void __launch_bounds__(NMBound<MAXM>::T) nm_fit_kernel(NMArgs a) {
             fn = __builtin_amdgcn_mov_dpp(fn, 0x150, 0xF, 0xF, false);   // row_newbcast:0
             f = fn;
             valid = fn < a.n_fits;
+            if (valid && a.jmajor && !a.coord) f = (fn % a.d) * nfc + fn / a.d;
             can_take = valid;
             start_fit();
         }
@@ -1389,6 +1395,10 @@ static int run_nm_parked(NMArgs a, hipStream_t st) {
     int32_t *cnt = (int32_t *)(park + a.n_fits);
     NNGP_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int32_t), st));
     a.park_cap = cap;
+    // jitter-major rows (NNGP_NM_JMAJOR=0: product order): fits sharing a jitter run similar
+    // evaluation counts, so a wave's rows finish together (d = 800 synthetic correction
+    // 2.99 -> 2.72 ms; profiles/r02/jmajor_probe.txt)
+    a.jmajor = getenv("NNGP_NM_JMAJOR") ? atoi(getenv("NNGP_NM_JMAJOR")) : 1;
     a.park = park;
     a.park_count = cnt;
     a.park_list = cnt + 1;
@@ -1587,6 +1597,7 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
     a.theta0 = theta0; a.fatol = fatol; a.xatol = xatol; a.maxfev = maxfev; a.R = n_restarts;
     a.fits_out = fits_out;
     a.qs_D2 = (int64_t)m * m; a.qs_Y = (int64_t)d * m; a.qs_th = (int64_t)nfp * 2; a.qs_fits = (int64_t)nfp * 4;
+    a.jmajor = getenv("NNGP_NM_JMAJOR") ? atoi(getenv("NNGP_NM_JMAJOR")) : 1;   // (run_nm_parked; Burgers 0.328 -> 0.317 s)
     // latency: a wave per fit (the re-speculation window the sweep waits on); else packed fits
     if (latency) return run_nm_spec(a, st, nq);
     return run_nm(a, false, st, nq);
