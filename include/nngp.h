@@ -193,7 +193,11 @@ int nngp_predict_range(const double *X, const double *Y, int64_t rows, int d, co
  *     a fit depends only on the ordered neighbours, coordinate, jitter and theta0), the others
  *     are recomputed in the sweep.  Auto speculates while (N-I)*d*n_jitter*n_restarts <= 262144.
  *   spec_hits_out: HOST, number of slices served by the speculative batch, or NULL;
- *   g_ms_out: HOST, total device time of the G launches (ms), or NULL (no timing events).    */
+ *   g_ms_out: HOST, total device time of the G launches (ms), or NULL (no timing events).
+ * With speculation on, an ODE or Burgers (d = 64k <= 256) system, exact G and m <= 32, the runs
+ * of hit slices go through ONE persistent cooperative kernel (G, kNN, hit check, arg-min, mean
+ * and update per slice, grid barriers between the phases; the host takes over at each miss):
+ * bitwise the launch chain.  NNGP_CHAIN=0 keeps the launch chain.                             */
 #define NNGP_MODEL_PARAREAL 0
 #define NNGP_MODEL_NNGP 1
 /* NNGP_MODEL_GPFULL: the full-data GP posterior mean (GPjax_p.predict, models.py:456-462) with
@@ -208,6 +212,11 @@ int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mode
                           const double *theta0, double fatol, double xatol, int maxfev,
                           double *preds_scratch, int speculate, int32_t *spec_hits_out, float *g_ms_out,
                           void *stream);
+
+/* Counters of the fused correction chain since the library was loaded (this process): kernel
+ * launches, and slices it completed (G through the update) -- the rest of the sweep's slices were
+ * misses finished by the host's fits.  Returns launches; *slices_out (HOST, optional). */
+int64_t nngp_chain_stats(int64_t *slices_out);
 
 /* ---- 4. full-data GParareal (models.GPjax_p, models.py:273-473) ------------------------------
  * The training set X, Y: DEVICE [rows][d], rows <= 7936.  K = sigma_y^2 exp(-0.5/sigma_x^2 D^2)

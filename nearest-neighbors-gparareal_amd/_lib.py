@@ -23,7 +23,7 @@ STEP_FIXED, STEP_LINSPACE, STEP_CONTRACT = 0, 1, 16
 EXPORTS = ['nngp_abi_version', 'nngp_last_error', 'nngp_device_count', 'nngp_rk_batch', 'nngp_rk_batch_grid',
            'nngp_rhs_batch', 'nngp_parareal_update', 'nngp_knn', 'nngp_nm_fit_batch',
            'nngp_gp_mean', 'nngp_predict', 'nngp_correction_sweep', 'nngp_gpfull_lml', 'nngp_gpfull_fit',
-           'nngp_gpfull_mean', 'nngp_predict_range']
+           'nngp_gpfull_mean', 'nngp_predict_range', 'nngp_chain_stats']
 MODEL_PARAREAL, MODEL_NNGP, MODEL_GPFULL = 0, 1, 2
 
 
@@ -79,10 +79,12 @@ def lib():
     L.nngp_gpfull_lml.argtypes = [_vp, i64, i32, _vp, i32, _ip, _dp, _dp, _dp, _vp, _vp]
     L.nngp_gpfull_fit.argtypes = [_vp, i64, i32, _vp, i32, _ip, _dp, _dp, dbl, dbl, i32, _dp, _dp, _ip, _ip, _vp]
     L.nngp_gpfull_mean.argtypes = [_vp, i64, i32, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.nngp_chain_stats.argtypes = [ctypes.POINTER(i64)]
+    L.nngp_chain_stats.restype = i64
     L.nngp_predict_range.argtypes = [_vp, _vp, i64, i32, _vp, i32, i32, _dp, i32, _vp, i32, i32, dbl, dbl, i32,
                                      _vp, _vp]
     for name in EXPORTS:
-        if name not in ('nngp_abi_version', 'nngp_last_error', 'nngp_device_count'):
+        if name not in ('nngp_abi_version', 'nngp_last_error', 'nngp_device_count', 'nngp_chain_stats'):
             getattr(L, name).restype = i32
     if L.nngp_abi_version() != 1:
         raise NNGPError('ABI version mismatch')
@@ -117,3 +119,11 @@ def as_device(a):
     if torch.is_tensor(a):
         return a.to(device='cuda', dtype=torch.float64).contiguous()
     return torch.tensor(np.ascontiguousarray(a, dtype=np.float64), device='cuda')
+
+
+def chain_stats():
+    """(fused-chain kernel launches, slices it completed) in this process (include/nngp.h)."""
+    L = lib()
+    sl = ctypes.c_int64(0)
+    n = L.nngp_chain_stats(ctypes.byref(sl))
+    return int(n), int(sl.value)

@@ -63,5 +63,15 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
                int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
                double fatol, double xatol, int maxfev, int32_t *idx_out, double *fits_out, bool latency,
                hipStream_t st);
+// the fused correction chain (nngp_gp.hip): one persistent kernel per run of hit slices
+bool chain_supported(const nngp_system *sys, int g_step_mode, int m);
+int chain_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps, const double *t, int I,
+                int N, int i0, double *U1, double *UG1, const double *X, const double *Y, int64_t rows, int m,
+                int n_jitter, const double *jitter_exp_host, int n_restarts, int32_t *flags,
+                const int32_t *spec_idx, const double *spec_fits, const int32_t *spec2_idx,
+                const double *spec2_fits, double *preds, int *stop_out, float *g_ms_out, hipStream_t st);
+int chain_miss_fits(int64_t rows, int d, int m, int n_jitter, const double *jitter_exp_host, int n_restarts,
+                    const double *theta0, double fatol, double xatol, int maxfev, double *preds,
+                    const double *bias, double *out, hipStream_t st);
 
 }  // namespace nngp

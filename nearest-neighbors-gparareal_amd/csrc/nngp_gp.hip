@@ -32,10 +32,12 @@
 #include <math.h>
 
 #include <algorithm>
+#include <mutex>
 
 #include "common.h"
 #include "nngp_math.h"
 #include "nngp_nm.h"
+#include "tableau.h"
 
 namespace nngp {
 
@@ -143,13 +145,9 @@ __device__ double pw_sqdiff(const double *__restrict__ a, const double *__restri
 // blockIdx.y = query (batched: query y is q + y*d, its distances dist + y*rows).
 // One lane per training row: the row is read with 16-byte vector loads that are all in flight at
 // once (no LDS staging, no barriers), then summed sequentially in column order (scipy cdist).
-__global__ void __launch_bounds__(64) knn_dist_kernel(const double *__restrict__ X, int64_t rows,
-                                                      int d, const double *__restrict__ q,
-                                                      double *__restrict__ dist) {
-    q += (size_t)blockIdx.y * d;
-    dist += (size_t)blockIdx.y * rows;
-    const int64_t r = (int64_t)blockIdx.x * 64 + threadIdx.x;
-    if (r >= rows) return;
+// squared distance of training row r to q (the kernel's and the correction chain's row body)
+__device__ __forceinline__ double knn_dist_row(const double *__restrict__ X, int d, const double *__restrict__ q,
+                                               int64_t r) {
     const double *xr = X + r * d;
     double acc = 0.0;
     int c = 0;
@@ -172,7 +170,17 @@ __global__ void __launch_bounds__(64) knn_dist_kernel(const double *__restrict__
         const double t = q[c] - xr[c];
         acc = acc + t * t;
     }
-    dist[r] = acc;
+    return acc;
+}
+
+__global__ void __launch_bounds__(64) knn_dist_kernel(const double *__restrict__ X, int64_t rows,
+                                                      int d, const double *__restrict__ q,
+                                                      double *__restrict__ dist) {
+    q += (size_t)blockIdx.y * d;
+    dist += (size_t)blockIdx.y * rows;
+    const int64_t r = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (r >= rows) return;
+    dist[r] = knn_dist_row(X, d, q, r);
 }
 
 __device__ __forceinline__ double wave_lane_double(double v, int lane) {
@@ -257,6 +265,16 @@ __device__ __forceinline__ void rank_merge(const uint64_t (*k)[64], const int (*
 static inline int knn_xs_doubles(int m, int64_t d) { return (int64_t)m * (d + 1) <= 6144 ? (int)(m * (d + 1)) : 0; }
 static inline size_t knn_xs_bytes(int m, int64_t d) { return (size_t)knn_xs_doubles(m, d) * sizeof(double); }
 
+// LDS of one select (the caller's: a kernel-level __shared__ object, one per kernel)
+struct SelShm {
+    int32_t sel[64];
+    double seld[64];
+    uint64_t rk[16][64];   // m <= 64
+    int ri[16][64];
+    uint64_t wk[4][64];
+    int wi[4][64];
+};
+
 template <int K> __global__ void knn_select_kernel(const double *, int64_t, int, const double *, const double *, int,
                                                   const double *, int32_t *, double *, double *, double *,
                                                   double *, const int32_t *, int32_t *, int, const int32_t *,
@@ -284,30 +302,22 @@ static void launch_knn_select(dim3 grid, size_t shmem, hipStream_t st, const dou
 // spec_idx, else 2 iff it equals spec2_idx (when given), else 0 -- the speculative sweep then
 // reuses the fits it computed for that list.  host_flag (host-mapped, optional) gets the same value.
 template <int K>
-__global__ void __launch_bounds__(256) knn_select_kernel(
-    const double *__restrict__ dist, int64_t rows, int m, const double *__restrict__ X,
+__device__ __forceinline__ void knn_select_dev(
+    SelShm &sh, const double *__restrict__ dist, int64_t rows, int m, const double *__restrict__ X,
     const double *__restrict__ Y, int d, const double *__restrict__ q, int32_t *__restrict__ idx_out,
     double *__restrict__ dist_out, double *__restrict__ ymT, double *__restrict__ D2,
     double *__restrict__ kd2, const int32_t *__restrict__ spec_idx, int32_t *__restrict__ hit_flag,
     int xs_doubles, const int32_t *__restrict__ spec2_idx, int32_t *host_flag) {
-    __shared__ int32_t sel[64];
-    __shared__ double seld[64];
-    const int qy = blockIdx.y;
-    dist += (size_t)qy * rows;
-    q += (size_t)qy * d;
-    idx_out += (size_t)qy * m;
-    if (dist_out) dist_out += (size_t)qy * m;
-    if (ymT) ymT += (size_t)qy * d * m;
-    if (D2) D2 += (size_t)qy * m * m;
-    if (kd2) kd2 += (size_t)qy * m;
+    int32_t *sel = sh.sel;
+    double *seld = sh.seld;
+    uint64_t(*rk)[64] = sh.rk;
+    int(*ri)[64] = sh.ri;
+    uint64_t(*wk)[64] = sh.wk;
+    int(*wi)[64] = sh.wi;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     // 1) each 16-lane row of the workgroup: its m best (key, index) pairs among its lanes' rows
     //    (row r of the training set belongs to thread r % 256), in ascending order, by m rounds of
     //    "smallest pair strictly after the previous pick" with a 4-level DPP row minimum
-    __shared__ uint64_t rk[16][64];   // m <= 64
-    __shared__ int ri[16][64];
-    __shared__ uint64_t wk[4][64];
-    __shared__ int wi[4][64];
     {
         const int grp = tid >> 4;
         // K > 0: the thread's K keys (rows tid + 256*j) stay in registers for all m rounds
@@ -359,20 +369,37 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
         idx_out[k] = sel[k];
         if (dist_out) dist_out[k] = seld[k];
     }
-    if (hit_flag && tid == 0) {
-        int hit1 = 1, hit2 = spec2_idx != nullptr;
-        for (int k = 0; k < m; k++) {
-            hit1 &= (sel[k] == spec_idx[k]);
-            if (spec2_idx) hit2 &= (sel[k] == spec2_idx[k]);
+    if (hit_flag && wid == 0) {   // lane k compares entry k of the lists: one round trip, not m
+        bool ne1 = false, ne2 = spec2_idx == nullptr;
+        for (int k = lane; k < m; k += 64) {
+            const int v = sel[k];
+            ne1 |= v != spec_idx[k];
+            if (spec2_idx) ne2 |= v != spec2_idx[k];
         }
+        const bool hit1 = __ballot(ne1) == 0, hit2 = __ballot(ne2) == 0;
         const int hit = hit1 ? 1 : (hit2 ? 2 : 0);
-        *hit_flag = hit;
-        if (host_flag) __hip_atomic_store(host_flag, hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lane == 0) {
+            *hit_flag = hit;
+            if (host_flag) __hip_atomic_store(host_flag, hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
+    // the gathers of the m selected rows: SG loads in flight per thread before their stores (a
+    // load -> store per trip would wait out one memory latency per element)
+    constexpr int SG = 8;
+    const int md = m * d;
     if (ymT) {   // coalesced row reads, transposed writes
-        for (int t = tid; t < m * d; t += 256) {
-            const int r = t / d, c = t - r * d;
-            ymT[c * m + r] = Y[(int64_t)sel[r] * d + c];
+        for (int t0 = tid; t0 < md; t0 += 256 * SG) {
+            double v[SG];
+#pragma unroll
+            for (int u = 0; u < SG; u++) {
+                const int t = t0 + 256 * u, r = t / d, c = t - r * d;
+                if (t < md) v[u] = Y[(int64_t)sel[r] * d + c];
+            }
+#pragma unroll
+            for (int u = 0; u < SG; u++) {
+                const int t = t0 + 256 * u, r = t / d, c = t - r * d;
+                if (t < md) ymT[c * m + r] = v[u];
+            }
         }
     }
     if (D2) {
@@ -383,13 +410,28 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
         const int ds = d + 1;
         const bool staged = (int64_t)m * ds <= xs_doubles;
         if (staged)
-            for (int t = tid; t < m * d; t += 256) {
-                const int r = t / d, c = t - r * d;
-                xs[r * ds + c] = X[(int64_t)sel[r] * d + c];
+            for (int t0 = tid; t0 < md; t0 += 256 * SG) {
+                double v[SG];
+#pragma unroll
+                for (int u = 0; u < SG; u++) {
+                    const int t = t0 + 256 * u, r = t / d, c = t - r * d;
+                    if (t < md) v[u] = X[(int64_t)sel[r] * d + c];
+                }
+#pragma unroll
+                for (int u = 0; u < SG; u++) {
+                    const int t = t0 + 256 * u, r = t / d, c = t - r * d;
+                    if (t < md) xs[r * ds + c] = v[u];
+                }
             }
         __syncthreads();
+        // the pairs, then kd2 on the next threads (one pass for m <= 21)
         const int npairs = m * (m + 1) / 2;
-        for (int t = tid; t < npairs; t += 256) {
+        for (int t = tid; t < npairs + (kd2 ? m : 0); t += 256) {
+            if (t >= npairs) {
+                const int r = t - npairs;
+                kd2[r] = pw_sqdiff(staged ? xs + (size_t)r * ds : X + (int64_t)sel[r] * d, q, d);
+                continue;
+            }
             int r = 0;
             while ((r + 1) * (r + 2) / 2 <= t) r++;
             const int j = t - r * (r + 1) / 2;
@@ -399,10 +441,27 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
             D2[r * m + j] = v;
             D2[j * m + r] = v;
         }
-        if (kd2)
-            for (int r = tid; r < m; r += 256)
-                kd2[r] = pw_sqdiff(staged ? xs + (size_t)r * ds : X + (int64_t)sel[r] * d, q, d);
     }
+}
+
+template <int K>
+__global__ void __launch_bounds__(256) knn_select_kernel(
+    const double *__restrict__ dist, int64_t rows, int m, const double *__restrict__ X,
+    const double *__restrict__ Y, int d, const double *__restrict__ q, int32_t *__restrict__ idx_out,
+    double *__restrict__ dist_out, double *__restrict__ ymT, double *__restrict__ D2,
+    double *__restrict__ kd2, const int32_t *__restrict__ spec_idx, int32_t *__restrict__ hit_flag,
+    int xs_doubles, const int32_t *__restrict__ spec2_idx, int32_t *host_flag) {
+    __shared__ SelShm sh;
+    const int qy = blockIdx.y;
+    dist += (size_t)qy * rows;
+    q += (size_t)qy * d;
+    idx_out += (size_t)qy * m;
+    if (dist_out) dist_out += (size_t)qy * m;
+    if (ymT) ymT += (size_t)qy * d * m;
+    if (D2) D2 += (size_t)qy * m * m;
+    if (kd2) kd2 += (size_t)qy * m;
+    knn_select_dev<K>(sh, dist, rows, m, X, Y, d, q, idx_out, dist_out, ymT, D2, kd2, spec_idx, hit_flag,
+                      xs_doubles, spec2_idx, host_flag);
 }
 
 // D2 / kd2 from an explicit xm (unfused entry points)
@@ -1154,17 +1213,21 @@ __global__ void __launch_bounds__(WGT<MAXM>::T) nm_spec_kernel(NMArgs a) {
 // (theta, jitter) either given (a.theta0[c], a.jitter_idx[c]: nngp_gp_mean) or the first arg-min
 // of the coordinate's a.nj*a.R fits in a.fits_out (the unfused nngp_predict path, used when a
 // coordinate's fits do not fit one workgroup).  Writes a.preds[c] and a.out[c] = mean (+ bias).
+// workgroup blk's coordinates (the kernel's blockIdx.x; the correction chain loops over them).
+// load_lds: stage D2/kd2 first (the chain stages them once per slice)
 template <int MAXM>
-__global__ void __launch_bounds__(WGT<MAXM>::T) gp_mean_kernel(NMArgs a) {
+__device__ __forceinline__ void gp_mean_dev(const NMArgs &a, int blk, bool load_lds) {
     constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG;
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int m = a.m, d = a.d;
     double *sD2 = sm, *skd2 = sm + m * m, *sK = skd2 + m;
     const int tid = threadIdx.x, g = tid / 16, l = tid % 16;
-    for (int i = tid; i < m * m; i += blockDim.x) sD2[i] = a.D2[i];
-    for (int i = tid; i < m; i += blockDim.x) skd2[i] = a.kd2[i];
-    __syncthreads();
-    const int c = blockIdx.x * (blockDim.x / 16) + g;
+    if (load_lds) {
+        for (int i = tid; i < m * m; i += blockDim.x) sD2[i] = a.D2[i];
+        for (int i = tid; i < m; i += blockDim.x) skd2[i] = a.kd2[i];
+        __syncthreads();
+    }
+    const int c = blk * (blockDim.x / 16) + g;
     const bool valid = c < d;
     const int cc = valid ? c : 0;
     double y[RPL];
@@ -1205,6 +1268,250 @@ __global__ void __launch_bounds__(WGT<MAXM>::T) gp_mean_kernel(NMArgs a) {
     if (valid && l == 0) {
         if (a.preds) a.preds[c] = mean;
         if (a.out) a.out[c] = a.bias ? mean + a.bias[c] : mean;
+    }
+}
+
+template <int MAXM>
+__global__ void __launch_bounds__(WGT<MAXM>::T) gp_mean_kernel(NMArgs a) {
+    gp_mean_dev<MAXM>(a, blockIdx.x, true);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused correction chain (reference parareal.py:359-382): the speculative
+// sweep's per-slice hit path as ONE persistent cooperative kernel.  For i = i0, i0+1, ...:
+//   1. G:      UG1[i+1] = G(U1[i])            workgroup 0 (one lane for an ODE, one wave for Burgers)
+//   2. kNN:    distances of every training row to U1[i]                    all workgroups
+//   3. select: the ordered m-neighbour list, y_m, D2, kd2; hit = list == the speculative batch's
+//              list (1) or the re-speculated one (2)                      workgroup 0
+//   4. on a hit: per coordinate the first arg-min over the batch's fits, the posterior mean and
+//              U1[i+1] = mean + UG1[i+1]                                  all workgroups
+// with a grid barrier between the phases.  A miss ends the kernel at slice i (its G and select
+// outputs are in the workspace) and the host runs that slice's fits; so the host sees one
+// round trip per MISS instead of ~5 launches and a host-flag wait per slice.  Every phase runs the
+// same device code as the unfused launches (lane_slice / burgers_wave_slice, knn_dist_row,
+// knn_select_dev, gp_mean_dev), so the sweep is bitwise unchanged.
+// ---------------------------------------------------------------------------------------------
+inline namespace exact {
+#include "nngp_rk_dev.h"
+}
+
+static constexpr int CHAIN_QMAX = 256;   // largest state the chain handles (Burgers d <= 256)
+
+struct ChainArgs {
+    NMArgs a;                  // the mean phase: m, d, nj, R, jit_pow; D2 / kd2 / Y = the workspace
+    LaneArgs la;               // G of an ODE (gkind 0)
+    FieldArgs fa;              // G of Burgers (gkind 1)
+    int gkind, sys, order, lin, norm, ept;
+    int64_t g_steps;
+    const double *t;           // [N+1] slice boundaries
+    int I, N, i0;
+    double *U1, *UG1;
+    const double *X, *Yd;      // training inputs / targets [rows][d]
+    int64_t rows;
+    int kk;                    // select variant (keys per thread: 2/4/8/16, 0 = streaming)
+    int xs_doubles;
+    int n_mean_blk;            // 16-lane coordinate groups / 16
+    double *dist;              // [rows]
+    int32_t *idx;              // [m]
+    int32_t *flags;            // [N-I] hit codes (0 = miss)
+    const int32_t *spec_idx, *spec2_idx;   // [N-I][m] (spec2: re-speculated lists, or null)
+    const double *spec_fits, *spec2_fits;  // [N-I][n_fits][4]
+    int64_t n_fits;
+    double *preds;             // [d]
+    uint32_t *bar;             // grid-barrier arrivals (zeroed before the launch)
+    int32_t *stop;             // host-mapped: the slice the chain stopped at (a miss), or N
+    uint64_t *g_ticks;         // host-mapped: wall-clock ticks spent in G
+    uint64_t *prof;            // host-mapped [4] or null (NNGP_CHAIN_PROF): ticks in G | kNN | select | mean
+};
+
+// all workgroups of the (cooperative, co-resident) grid: arrivals counted on one agent-scope
+// counter; the fences make every workgroup's global writes before the barrier visible to every
+// workgroup after it (L2 write-back / invalidate across the XCDs)
+__device__ __forceinline__ void chain_barrier(uint32_t *bar, uint32_t &target) {
+    __syncthreads();
+    if (gridDim.x == 1) return;
+    target += gridDim.x;
+    if (threadIdx.x == 0) {
+        __threadfence();
+        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target)
+            __builtin_amdgcn_s_sleep(1);
+        __threadfence();
+    }
+    __syncthreads();
+}
+
+template <int SYS, int ORDER>
+__device__ __forceinline__ void chain_lane_g2(const LaneArgs &la, bool lin, bool norm, double T0, double T1,
+                                              int64_t steps, const double *u0, double *out) {
+    if (lin) {
+        if (norm) lane_slice<SYS, ORDER, true, true>(la, T0, T1, steps, steps, 0, u0, out);
+        else lane_slice<SYS, ORDER, true, false>(la, T0, T1, steps, steps, 0, u0, out);
+    } else {
+        if (norm) lane_slice<SYS, ORDER, false, true>(la, T0, T1, steps, steps, 0, u0, out);
+        else lane_slice<SYS, ORDER, false, false>(la, T0, T1, steps, steps, 0, u0, out);
+    }
+}
+
+template <int SYS>
+__device__ __forceinline__ void chain_lane_g1(const LaneArgs &la, int order, bool lin, bool norm, double T0,
+                                              double T1, int64_t steps, const double *u0, double *out) {
+    switch (order) {
+    case 1: chain_lane_g2<SYS, 1>(la, lin, norm, T0, T1, steps, u0, out); break;
+    case 2: chain_lane_g2<SYS, 2>(la, lin, norm, T0, T1, steps, u0, out); break;
+    case 4: chain_lane_g2<SYS, 4>(la, lin, norm, T0, T1, steps, u0, out); break;
+    default: chain_lane_g2<SYS, 8>(la, lin, norm, T0, T1, steps, u0, out); break;
+    }
+}
+
+// G of one ODE slice by one lane (the G launch's lane form; bitwise its group form), compiled
+// once and called from every chain instantiation
+__device__ __attribute__((noinline)) void chain_lane_g(LaneArgs la, int sys, int order, int lin, int norm,
+                                                       double T0, double T1, int64_t steps, const double *u0,
+                                                       double *out) {
+    switch (sys) {
+    case NNGP_SYS_LORENZ: chain_lane_g1<NNGP_SYS_LORENZ>(la, order, lin, norm, T0, T1, steps, u0, out); break;
+    case NNGP_SYS_HOPF: chain_lane_g1<NNGP_SYS_HOPF>(la, order, lin, norm, T0, T1, steps, u0, out); break;
+    case NNGP_SYS_THOMAS_LABYRINTH:
+        chain_lane_g1<NNGP_SYS_THOMAS_LABYRINTH>(la, order, lin, norm, T0, T1, steps, u0, out);
+        break;
+    case NNGP_SYS_FHN_ODE: chain_lane_g1<NNGP_SYS_FHN_ODE>(la, order, lin, norm, T0, T1, steps, u0, out); break;
+    case NNGP_SYS_ROSSLER: chain_lane_g1<NNGP_SYS_ROSSLER>(la, order, lin, norm, T0, T1, steps, u0, out); break;
+    case NNGP_SYS_BRUSSELATOR:
+        chain_lane_g1<NNGP_SYS_BRUSSELATOR>(la, order, lin, norm, T0, T1, steps, u0, out);
+        break;
+    default: chain_lane_g1<NNGP_SYS_DBL_PEND>(la, order, lin, norm, T0, T1, steps, u0, out); break;
+    }
+}
+
+template <int ORDER, int EPT>
+__device__ __forceinline__ void chain_burgers_g2(const FieldArgs &fa, bool lin, bool norm, int l, double T0,
+                                                 double T1, int64_t steps, const double *u0, double *out) {
+    if (lin) {
+        if (norm) burgers_wave_slice<ORDER, true, EPT, true>(fa, l, T0, T1, steps, steps, 0, u0, out);
+        else burgers_wave_slice<ORDER, true, EPT, false>(fa, l, T0, T1, steps, steps, 0, u0, out);
+    } else {
+        if (norm) burgers_wave_slice<ORDER, false, EPT, true>(fa, l, T0, T1, steps, steps, 0, u0, out);
+        else burgers_wave_slice<ORDER, false, EPT, false>(fa, l, T0, T1, steps, steps, 0, u0, out);
+    }
+}
+
+template <int EPT>
+__device__ __forceinline__ void chain_burgers_g1(const FieldArgs &fa, int order, bool lin, bool norm, int l,
+                                                 double T0, double T1, int64_t steps, const double *u0,
+                                                 double *out) {
+    switch (order) {
+    case 1: chain_burgers_g2<1, EPT>(fa, lin, norm, l, T0, T1, steps, u0, out); break;
+    case 2: chain_burgers_g2<2, EPT>(fa, lin, norm, l, T0, T1, steps, u0, out); break;
+    case 4: chain_burgers_g2<4, EPT>(fa, lin, norm, l, T0, T1, steps, u0, out); break;
+    default: chain_burgers_g2<8, EPT>(fa, lin, norm, l, T0, T1, steps, u0, out); break;
+    }
+}
+
+// G of one Burgers slice by one full wave (the G launch's wave form)
+__device__ __attribute__((noinline)) void chain_burgers_g(FieldArgs fa, int ept, int order, int lin, int norm,
+                                                          int l, double T0, double T1, int64_t steps,
+                                                          const double *u0, double *out) {
+    switch (ept) {
+    case 1: chain_burgers_g1<1>(fa, order, lin, norm, l, T0, T1, steps, u0, out); break;
+    case 2: chain_burgers_g1<2>(fa, order, lin, norm, l, T0, T1, steps, u0, out); break;
+    case 3: chain_burgers_g1<3>(fa, order, lin, norm, l, T0, T1, steps, u0, out); break;
+    default: chain_burgers_g1<4>(fa, order, lin, norm, l, T0, T1, steps, u0, out); break;
+    }
+}
+
+template <int MAXM>
+__global__ void __launch_bounds__(256) chain_kernel(ChainArgs c) {
+    __shared__ SelShm sh;
+    __shared__ __attribute__((aligned(16))) double qs[CHAIN_QMAX];   // U1[i], read once per slice
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+    const int d = c.a.d, m = c.a.m;
+    uint32_t target = 0;
+    uint64_t g_ticks = 0, pt[4] = {0, 0, 0, 0}, tp = 0;
+    const bool prof = c.prof != nullptr && blockIdx.x == 0;
+#define CHAIN_MARK(k)                          \
+    if (prof) {                                \
+        const uint64_t now = wall_clock64();   \
+        pt[k] += now - tp;                     \
+        tp = now;                              \
+    }
+    int i = c.i0;
+    for (; i < c.N; i++) {
+        const size_t j = (size_t)(i - c.I);
+        const double *ui = c.U1 + (size_t)i * d;
+        double *ug_next = c.UG1 + (size_t)(i + 1) * d;
+        double *u_next = c.U1 + (size_t)(i + 1) * d;
+        // U1[i] was written by the previous slice's mean phase (another workgroup): atomic loads
+        // keep the read on the vector path, past the barrier's cache invalidation
+        if (prof) tp = wall_clock64();
+        for (int e = tid; e < d; e += 256)
+            qs[e] = __hip_atomic_load(ui + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        // 1) G
+        if (blockIdx.x == 0) {
+            const uint64_t w0 = wall_clock64();
+            if (c.gkind == 0) {
+                if (tid == 0)
+                    chain_lane_g(c.la, c.sys, c.order, c.lin, c.norm, c.t[i], c.t[i + 1], c.g_steps, qs, ug_next);
+            } else if (wid == 0) {
+                chain_burgers_g(c.fa, c.ept, c.order, c.lin, c.norm, lane, c.t[i], c.t[i + 1], c.g_steps, qs,
+                                ug_next);
+            }
+            __syncthreads();
+            g_ticks += wall_clock64() - w0;
+            CHAIN_MARK(0);
+        }
+        // 2) distances of every training row (grid-stride over the workgroups)
+        for (int64_t r = (int64_t)blockIdx.x * 256 + tid; r < c.rows; r += (int64_t)gridDim.x * 256)
+            c.dist[r] = knn_dist_row(c.X, d, qs, r);
+        chain_barrier(c.bar, target);
+        CHAIN_MARK(1);
+        // 3) ordered neighbour list, y_m, D2, kd2 and the hit code
+        if (blockIdx.x == 0) {
+            const int32_t *s2 = c.spec2_idx ? c.spec2_idx + j * m : nullptr;
+            const int32_t *s1 = c.spec_idx + j * m;
+            int32_t *fl = c.flags + j;
+            double *ymT = const_cast<double *>(c.a.Y);
+            double *D2 = const_cast<double *>(c.a.D2), *kd2 = const_cast<double *>(c.a.kd2);
+            switch (c.kk) {
+            case 2: knn_select_dev<2>(sh, c.dist, c.rows, m, c.X, c.Yd, d, qs, c.idx, nullptr, ymT, D2, kd2, s1, fl,
+                                      c.xs_doubles, s2, nullptr); break;
+            case 4: knn_select_dev<4>(sh, c.dist, c.rows, m, c.X, c.Yd, d, qs, c.idx, nullptr, ymT, D2, kd2, s1, fl,
+                                      c.xs_doubles, s2, nullptr); break;
+            case 8: knn_select_dev<8>(sh, c.dist, c.rows, m, c.X, c.Yd, d, qs, c.idx, nullptr, ymT, D2, kd2, s1, fl,
+                                      c.xs_doubles, s2, nullptr); break;
+            case 16: knn_select_dev<16>(sh, c.dist, c.rows, m, c.X, c.Yd, d, qs, c.idx, nullptr, ymT, D2, kd2, s1,
+                                        fl, c.xs_doubles, s2, nullptr); break;
+            default: knn_select_dev<0>(sh, c.dist, c.rows, m, c.X, c.Yd, d, qs, c.idx, nullptr, ymT, D2, kd2, s1,
+                                       fl, c.xs_doubles, s2, nullptr); break;
+            }
+        }
+        chain_barrier(c.bar, target);
+        CHAIN_MARK(2);
+        const int hit = __hip_atomic_load(c.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (hit == 0) break;   // uniform over the grid: the host runs this slice's fits
+        // 4) arg-min over the batch's fits, posterior mean, U1[i+1] = mean + UG1[i+1]
+        NMArgs a = c.a;   // the hit's fits, as gp_mean_kernel picks them through a.skip
+        a.skip = nullptr;
+        a.fits_out = const_cast<double *>(hit == 2 ? c.spec2_fits : c.spec_fits) + j * c.n_fits * 4;
+        a.bias = ug_next;
+        a.out = u_next;
+        a.preds = c.preds;
+        bool first = true;
+        for (int blk = blockIdx.x; blk < c.n_mean_blk; blk += gridDim.x) {
+            if (!first) __syncthreads();
+            gp_mean_dev<MAXM>(a, blk, first);
+            first = false;
+        }
+        chain_barrier(c.bar, target);
+        CHAIN_MARK(3);
+    }
+#undef CHAIN_MARK
+    if (prof && tid == 0)
+        for (int k = 0; k < 4; k++) __hip_atomic_store(c.prof + k, pt[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (blockIdx.x == 0 && tid == 0) {
+        __hip_atomic_store(c.g_ticks, g_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(c.stop, i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1603,7 +1910,207 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
     return run_nm(a, false, st, nq);
 }
 
+// ---- the fused correction chain, host side ----------------------------------------------------
+struct ChainRes {
+    int dev = -1;
+    int coop = 0;             // cooperative launches supported
+    double tick_khz = 0;      // wall_clock64 rate
+    uint32_t *bar = nullptr;  // device: grid-barrier counter
+    int32_t *stop = nullptr;  // host-mapped: stop slice | G ticks (u64)
+};
+static ChainRes g_chain;
+static std::mutex g_chain_mu;
+static int64_t g_chain_launches = 0, g_chain_slices = 0;   // nngp_chain_stats (under g_chain_mu)
+
+static int chain_resources(ChainRes **out) {
+    std::lock_guard<std::mutex> lk(g_chain_mu);
+    ChainRes &r = g_chain;
+    int dev = 0;
+    NNGP_HIP_CHECK(hipGetDevice(&dev));
+    if (r.dev != dev) {
+        if (r.bar) (void)hipFree(r.bar);
+        if (r.stop) (void)hipHostFree(r.stop);
+        r = ChainRes{};
+        NNGP_HIP_CHECK(hipDeviceGetAttribute(&r.coop, hipDeviceAttributeCooperativeLaunch, dev));
+        int khz = 0;
+        NNGP_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+        r.tick_khz = khz > 0 ? khz : 100000.0;
+        NNGP_HIP_CHECK(hipMalloc((void **)&r.bar, 256));
+        NNGP_HIP_CHECK(hipHostMalloc((void **)&r.stop, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        r.dev = dev;
+    }
+    *out = &r;
+    return NNGP_OK;
+}
+
+// the systems / shapes the chain's in-kernel G covers (the rest keep the launch chain):
+// every ODE (lane form) and Burgers with d = 64*EPT <= 256 (wave form); exact G, m <= 32.
+// NNGP_CHAIN=0 disables it (A/B).
+bool chain_supported(const nngp_system *sys, int g_step_mode, int m) {
+    const char *e = getenv("NNGP_CHAIN");
+    if (e && atoi(e) == 0) return false;
+    if (g_step_mode & NNGP_STEP_CONTRACT) return false;
+    if (m < 1 || m > 32 || sys->d > CHAIN_QMAX) return false;
+    switch (sys->kind) {
+    case NNGP_SYS_LORENZ: case NNGP_SYS_HOPF: case NNGP_SYS_THOMAS_LABYRINTH: case NNGP_SYS_FHN_ODE:
+    case NNGP_SYS_ROSSLER: case NNGP_SYS_BRUSSELATOR: case NNGP_SYS_DBL_PEND:
+        return true;
+    case NNGP_SYS_BURGERS:
+        return sys->nx == sys->d && sys->d % 64 == 0 && sys->d <= 256;
+    default:
+        return false;
+    }
+}
+
+template <int MAXM>
+static int chain_launch(ChainArgs &c, int nb, size_t lds, hipStream_t st) {
+    void *args[] = {&c};
+    NNGP_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&chain_kernel<MAXM>), dim3(nb),
+                                              dim3(256), args, (unsigned)lds, st));
+    return NNGP_OK;
+}
+
+// Run the chain from slice i0 on stream st until the first miss (or N).  *stop_out = that slice:
+// its G output (UG1[stop+1]) and its select workspace (chain_miss_fits) are in place.  The call
+// returns after the kernel has drained; *g_ms_out += the in-kernel G time.
+int chain_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps, const double *t, int I,
+                int N, int i0, double *U1, double *UG1, const double *X, const double *Y, int64_t rows, int m,
+                int n_jitter, const double *jitter_exp_host, int n_restarts, int32_t *flags,
+                const int32_t *spec_idx, const double *spec_fits, const int32_t *spec2_idx,
+                const double *spec2_fits, double *preds, int *stop_out, float *g_ms_out, hipStream_t st) {
+    const int d = sys->d;
+    NNGP_REQUIRE(chain_supported(sys, g_step_mode, m) && I <= i0 && i0 < N && m <= rows, "chain: unsupported shape");
+    ChainRes *res = nullptr;
+    int rc = chain_resources(&res);
+    if (rc) return rc;
+    NNGP_REQUIRE(res->coop, "chain: cooperative launches unsupported on this device");
+    ChainArgs c{};
+    rc = fill_jitters(c.a, n_jitter, jitter_exp_host);
+    if (rc) return rc;
+    // slot-0 workspace, predict_impl's layout: dist[rows] | D2[m*m] | kd2[m] | ymT[d*m] | idx[64] | fits
+    const size_t nd = (size_t)rows + (size_t)m * m + m + (size_t)d * m;
+    const size_t n_fits = (size_t)d * n_jitter * n_restarts;
+    int err = 0;
+    char *ws = (char *)workspace(sizeof(double) * nd + sizeof(int32_t) * 64 + sizeof(double) * 4 * n_fits, &err);
+    if (err) return err;
+    double *dist = (double *)ws;
+    double *D2 = dist + rows, *kd2 = D2 + (size_t)m * m, *ymT = kd2 + m;
+    c.a.m = m; c.a.d = d; c.a.n_fits = (int)n_fits; c.a.D2 = D2; c.a.kd2 = kd2; c.a.Y = ymT;
+    c.a.ys_c = m; c.a.ys_r = 1; c.a.R = n_restarts;
+    const int kind = sys->kind;
+    if (kind == NNGP_SYS_BURGERS) {
+        c.gkind = 1;
+        c.ept = d / 64;
+        c.fa.d = d; c.fa.nx = sys->nx; c.fa.normalized = sys->normalized; c.fa.norm = sys->norm;
+        const double dx = (1.0 - (-1.0)) / (sys->d - 1);   // as field_args (nngp_rk_dev.h users)
+        const double nu = sys->param[0];
+        c.fa.c_off = nu / (dx * dx);
+        c.fa.c_diag = c.fa.c_off * -2.0;
+        c.fa.c_grad = 1 / (2 * dx);
+    } else {
+        c.gkind = 0;
+        c.la.normalized = sys->normalized;
+        for (int k = 0; k < 4; k++) c.la.param[k] = sys->param[k];
+        c.la.rparam0 = 1.0 / sys->param[0];
+        c.la.norm = sys->norm;
+    }
+    NNGP_REQUIRE(!sys->normalized || sys->norm, "normalized system needs norm[3d]");
+    NNGP_REQUIRE(g_tableau == 1 || g_tableau == 2 || g_tableau == 4 || g_tableau == 8, "bad G tableau %d", g_tableau);
+    c.sys = kind; c.order = g_tableau;
+    c.lin = (g_step_mode & ~NNGP_STEP_CONTRACT) == NNGP_STEP_LINSPACE;
+    c.norm = sys->normalized != 0;
+    c.g_steps = g_steps;
+    c.t = t; c.I = I; c.N = N; c.i0 = i0;
+    c.U1 = U1; c.UG1 = UG1; c.X = X; c.Yd = Y; c.rows = rows;
+    const int64_t per = (rows + 255) / 256;
+    c.kk = per <= 2 ? 2 : (per <= 4 ? 4 : (per <= 8 ? 8 : (per <= 16 ? 16 : 0)));
+    c.xs_doubles = knn_xs_doubles(m, d);
+    c.n_mean_blk = (d + 15) / 16;
+    c.dist = dist; c.idx = (int32_t *)(ymT + (size_t)d * m);
+    c.flags = flags; c.spec_idx = spec_idx; c.spec2_idx = spec2_idx;
+    c.spec_fits = spec_fits; c.spec2_fits = spec2_fits; c.n_fits = (int64_t)n_fits;
+    c.preds = preds;
+    c.bar = res->bar;
+    c.stop = res->stop;
+    c.g_ticks = (uint64_t *)(res->stop + 2);
+    static const bool prof = getenv("NNGP_CHAIN_PROF") && atoi(getenv("NNGP_CHAIN_PROF"));
+    c.prof = prof ? (uint64_t *)(res->stop + 4) : nullptr;
+    const int maxm = maxm_for(m);
+    const size_t lds = std::max(knn_xs_bytes(m, d),
+                                sizeof(double) * ((size_t)m * m + m + 16 * k_image_doubles(maxm)));
+    NNGP_REQUIRE(lds + sizeof(SelShm) + sizeof(double) * CHAIN_QMAX <= 160 * 1024, "chain: LDS");
+    const int nb = std::max(1, std::min(c.n_mean_blk, 64));
+    res->stop[0] = -1;
+    NNGP_HIP_CHECK(hipMemsetAsync(res->bar, 0, sizeof(uint32_t), st));
+    switch (maxm) {
+    case 8: rc = chain_launch<8>(c, nb, lds, st); break;
+    case 16: rc = chain_launch<16>(c, nb, lds, st); break;
+    case 20: rc = chain_launch<20>(c, nb, lds, st); break;
+    case 24: rc = chain_launch<24>(c, nb, lds, st); break;
+    default: rc = chain_launch<32>(c, nb, lds, st); break;
+    }
+    if (rc) return rc;
+    NNGP_HIP_CHECK(hipStreamSynchronize(st));
+    const int stop = __atomic_load_n(res->stop, __ATOMIC_ACQUIRE);
+    if (stop < i0 || stop > N) {
+        set_error("chain: the kernel reported no stop slice (%d)", stop);
+        return NNGP_E_HIP;
+    }
+    *stop_out = stop;
+    if (g_ms_out) *g_ms_out += (float)((double)*c.g_ticks / res->tick_khz);
+    if (c.prof)
+        fprintf(stderr, "chain i0=%d stop=%d d=%d rows=%lld nb=%d us: G %.1f kNN %.1f select %.1f mean %.1f\n", i0,
+                stop, d, (long long)rows, nb, c.prof[0] / res->tick_khz * 1e3, c.prof[1] / res->tick_khz * 1e3,
+                c.prof[2] / res->tick_khz * 1e3, c.prof[3] / res->tick_khz * 1e3);
+    {
+        std::lock_guard<std::mutex> lk(g_chain_mu);
+        g_chain_launches++;
+        g_chain_slices += stop - i0;
+    }
+    return NNGP_OK;
+}
+
+// The fits of the slice the chain stopped at (a miss), from the chain's select workspace, then
+// the arg-min, mean and U1[stop+1] = mean + UG1[stop+1]: predict_impl's launches after its select
+// on a speculation miss, so the result is bitwise the unfused sweep's.
+int chain_miss_fits(int64_t rows, int d, int m, int n_jitter, const double *jitter_exp_host, int n_restarts,
+                    const double *theta0, double fatol, double xatol, int maxfev, double *preds,
+                    const double *bias, double *out, hipStream_t st) {
+    NMArgs a{};
+    int rc = fill_jitters(a, n_jitter, jitter_exp_host);
+    if (rc) return rc;
+    const size_t nd = (size_t)rows + (size_t)m * m + m + (size_t)d * m;
+    const size_t n_fits = (size_t)d * n_jitter * n_restarts;
+    int err = 0;
+    char *ws = (char *)workspace(sizeof(double) * nd + sizeof(int32_t) * 64 + sizeof(double) * 4 * n_fits, &err);
+    if (err) return err;
+    double *D2 = (double *)ws + rows, *kd2 = D2 + (size_t)m * m, *ymT = kd2 + m;
+    double *fits_ws = (double *)(ws + sizeof(double) * nd + sizeof(int32_t) * 64);
+    a.m = m; a.d = d; a.n_fits = (int)n_fits;
+    a.D2 = D2; a.kd2 = kd2; a.Y = ymT; a.ys_c = m; a.ys_r = 1;
+    a.theta0 = theta0; a.fatol = fatol; a.xatol = xatol; a.maxfev = maxfev;
+    a.R = n_restarts;
+    a.fits_out = fits_ws;
+    a.preds = preds; a.bias = bias; a.out = out;
+    if (use_spec(a.n_fits, a.m)) {
+        rc = run_nm_spec(a, st);
+        if (rc) return rc;
+        return run_mean(a, st);
+    }
+    NMArgs u = a;
+    u.preds = nullptr; u.out = nullptr; u.bias = nullptr;
+    rc = run_nm_parked(u, st);
+    if (rc) return rc;
+    return run_mean(a, st);
+}
+
 }  // namespace nngp
+
+extern "C" int64_t nngp_chain_stats(int64_t *slices_out) {
+    std::lock_guard<std::mutex> lk(nngp::g_chain_mu);
+    if (slices_out) *slices_out = nngp::g_chain_slices;
+    return nngp::g_chain_launches;
+}
 
 extern "C" int nngp_predict(const double *X, const double *Y, int64_t rows, int d, const double *new_x,
                             int m, int n_jitter, const double *jitter_exp_host, int n_restarts,

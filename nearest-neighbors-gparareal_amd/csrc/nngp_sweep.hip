@@ -212,7 +212,53 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
         if (rc) return rc;
     }
     bool respec_pending = false;
-    for (int i = I; i < N && rc == NNGP_OK; i++) {
+    // ---- the fused chain (nngp_gp.hip chain_kernel): runs of hit slices as one persistent kernel;
+    // the host takes over at each miss (that slice's fits, the re-speculation), then resumes it
+    const bool chained = spec && chain_supported(sys, g_step_mode, m);
+    if (chained) {
+        float g_ms = 0.f;
+        int i = I;
+        while (i < N && rc == NNGP_OK) {
+            if (respec_pending) NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_r, 0));   // lists/fits ready
+            respec_pending = false;
+            int s = N;
+            rc = chain_sweep(sys, g_tableau, g_step_mode, g_steps, t, I, N, i, U1, UG1, X, Y, rows, m, n_jitter,
+                             jitter_exp_host, n_restarts, flags, spec_idx, spec_fits, W > 0 ? spec2_idx : nullptr,
+                             W > 0 ? spec2_fits : nullptr, preds_scratch, &s, &g_ms, st);
+            if (rc || s >= N) break;
+            // miss at slice s: G(U1[s]) and its select are done (the chain kernel has drained)
+            const size_t j = (size_t)(s - I);
+            double *ug_next = UG1 + (size_t)(s + 1) * d;
+            rc = chain_miss_fits(rows, d, m, n_jitter, jitter_exp_host, n_restarts, theta0 + j * n_fits * 2, fatol,
+                                 xatol, maxfev, preds_scratch, ug_next, U1 + (size_t)(s + 1) * d, st);
+            if (rc == NNGP_OK && W > 0 && s + 1 < N) {   // re-guess slices s+1 .. s+w from U1[s]
+                const int w = (int)std::min<int64_t>(W, N - 1 - s);
+                hipStream_t s2 = rs->st2;
+                double *g2 = Qr + (size_t)W * d;
+                rc = nngp_parareal_update(d, UF + (size_t)(s + 1) * d, UG + (size_t)(s + 1) * d, ug_next, Qr, s2);
+                for (int q = 1; q < w && rc == NNGP_OK; q++) {
+                    const int sq = s + q;
+                    rc = nngp_rk_batch(sys, g_tableau, g_step_mode, 1, t + sq, t + sq + 1, g_steps,
+                                       Qr + (size_t)(q - 1) * d, g2, s2);
+                    if (rc == NNGP_OK)
+                        rc = nngp_parareal_update(d, UF + (size_t)(sq + 1) * d, UG + (size_t)(sq + 1) * d, g2,
+                                                  Qr + (size_t)q * d, s2);
+                }
+                if (rc == NNGP_OK)
+                    rc = spec_batch(X, Y, rows, d, Qr, w, m, n_jitter, jitter_exp_host, n_restarts,
+                                    theta0 + (j + 1) * n_fits * 2, fatol, xatol, maxfev, spec2_idx + (j + 1) * m,
+                                    spec2_fits + (j + 1) * n_fits * 4, env_int("NNGP_RESPEC_PACKED", 0) == 0, s2);
+                if (rc == NNGP_OK) {
+                    NNGP_HIP_CHECK(hipEventRecord(rs->ev_r, s2));
+                    respec_pending = true;
+                }
+            }
+            i = s + 1;
+        }
+        if (g_ms_out && rc == NNGP_OK) *g_ms_out = g_ms;
+        ev = nullptr;   // G time comes from the chain's clock
+    }
+    for (int i = chained ? N : I; i < N && rc == NNGP_OK; i++) {   // the launch chain
         const double *ui = U1 + (size_t)i * d;
         double *ug_next = UG1 + (size_t)(i + 1) * d;
         double *u_next = U1 + (size_t)(i + 1) * d;

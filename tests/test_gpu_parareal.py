@@ -230,3 +230,62 @@ def test_hopf_n128_nngp_bitwise_equals_oracle_loop(gpu, F):
     print('Hopf N=128', F, 'K', r['k'], 'conv_int', r['conv_int'], 'spec hits', r['timings']['spec_hits'])
     assert r['converged'] and r['k'] == o['k'] and r['conv_int'] == o['conv_int']
     assert np.array_equal(np.nan_to_num(r['u'], nan=7.0), np.nan_to_num(o['u'], nan=7.0))
+
+
+def _chain_case(gpu, case):
+    """(Parareal, run kwargs) for the fused-chain A/B cases: Burgers (wave G, RK1), Lorenz (RK4 G),
+    FHN-ODE (RK2 G, d=2), Hopf (RK1, 2 restarts), Burgers without normalisation, the legacy
+    linspace-grid Lorenz and double pendulum (d=4, sincos G)."""
+    if case == 'burgers':
+        ode = gpu.Burgers(d_x=128, normalization='-11')
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
+        return gpu.Parareal(ode, s, [0, 5], 128, epsilon=5e-7, verbose=None), dict(nn=15, seed=45, early_stop=3)
+    if case == 'burgers_raw':
+        ode = gpu.Burgers(d_x=64)
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=4, Nf=1000, F='RK4', G='RK2')
+        return gpu.Parareal(ode, s, [0, 5], 64, epsilon=5e-7, verbose=None), dict(nn=12, seed=46, early_stop=3)
+    if case == 'lorenz':
+        ode = gpu.Lorenz(normalization='-11')
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=6, Nf=450, F='RK4', G='RK4')
+        return gpu.Parareal(ode, s, [0, 18], 32, epsilon=5e-7, verbose=None), dict(nn=10, seed=47)
+    if case == 'lorenz_linspace':
+        ode = gpu.Lorenz(normalization='-11')
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=6, Nf=450, F='RK4', G='RK4', step_mode='linspace')
+        return gpu.Parareal(ode, s, [0, 18], 32, epsilon=5e-7, verbose=None), dict(nn=10, seed=45)
+    if case == 'fhn_ode':
+        ode = gpu.FHN_ODE(normalization='-11')
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=4, Nf=4000, F='RK4', G='RK2')
+        return gpu.Parareal(ode, s, [0, 40], 40, epsilon=5e-7, verbose=None), dict(nn=15, seed=45)
+    if case == 'hopf':
+        ode = gpu.Hopf(normalization='-11')
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=16, Nf=1360, F='RK4', G='RK1')
+        return (gpu.Parareal(ode, s, [-20, 500], 64, epsilon=5e-7, verbose=None),
+                dict(nn=15, n_restarts=2, fatol=0.1, xatol=0.1, seed=45, early_stop=4))
+    ode = gpu.DblPend(normalization='-11')
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=12, Nf=800, F='RK8', G='RK1')
+    return gpu.Parareal(ode, s, [0, 16], 32, epsilon=5e-7, verbose=None), dict(nn=12, seed=45, early_stop=4)
+
+
+@pytest.mark.parametrize('case', ['burgers', 'burgers_raw', 'lorenz', 'lorenz_linspace', 'fhn_ode', 'hopf',
+                                  'dblpend'])
+def test_fused_chain_is_bitwise_the_launch_chain(gpu, case, monkeypatch):
+    """the runs of speculation hits go through one persistent kernel per run
+    (G, kNN, hit check, arg-min, posterior mean and u = pred + uG per slice; the host takes over at
+    each miss).  Every iterate, K, conv_int, the hit counts and the G-time key match the unfused
+    launch chain (NNGP_CHAIN=0) bit for bit, and the chain really ran."""
+    from nngp_amd import _lib
+    p, kw = _chain_case(gpu, case)
+    monkeypatch.setenv('NNGP_CHAIN', '0')
+    n0, s0 = _lib.chain_stats()
+    a = p.run(model='nngp', speculate=1, **kw)
+    assert _lib.chain_stats() == (n0, s0)
+    monkeypatch.setenv('NNGP_CHAIN', '1')
+    b = p.run(model='nngp', speculate=1, **kw)
+    n1, s1 = _lib.chain_stats()
+    print(case, 'K', b['k'], 'hits', b['timings']['spec_hits'], 'chain launches', n1 - n0, 'slices', s1 - s0,
+          'G ms', a['timings']['G_time'] * 1e3, b['timings']['G_time'] * 1e3)
+    assert a['k'] == b['k'] and a['conv_int'] == b['conv_int']
+    assert a['timings']['spec_hits'] == b['timings']['spec_hits']
+    assert np.array_equal(np.nan_to_num(a['u'], nan=7.0), np.nan_to_num(b['u'], nan=7.0))
+    assert n1 > n0 and s1 - s0 == sum(b['timings']['spec_hits'])
+    assert b['timings']['G_time'] > 0
