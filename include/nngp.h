@@ -194,10 +194,11 @@ int nngp_predict_range(const double *X, const double *Y, int64_t rows, int d, co
  *     are recomputed in the sweep.  Auto speculates while (N-I)*d*n_jitter*n_restarts <= 262144.
  *   spec_hits_out: HOST, number of slices served by the speculative batch, or NULL;
  *   g_ms_out: HOST, total device time of the G launches (ms), or NULL (no timing events).
- * With speculation on, an ODE or Burgers (d = 64k <= 256) system, exact G and m <= 32, the runs
+ * With NNGP_CHAIN=1, speculation on, an ODE or Burgers (d = 64k <= 256) system, exact G and m <= 32, the runs
  * of hit slices go through ONE persistent cooperative kernel (G, kNN, hit check, arg-min, mean
  * and update per slice, grid barriers between the phases; the host takes over at each miss):
- * bitwise the launch chain.  NNGP_CHAIN=0 keeps the launch chain.                             */
+ * bitwise the launch chain.  Opt-in (NNGP_CHAIN=1): measured not faster than the launch chain
+ * on MI355X, so the launch chain stays the default.                        */
 #define NNGP_MODEL_PARAREAL 0
 #define NNGP_MODEL_NNGP 1
 /* NNGP_MODEL_GPFULL: the full-data GP posterior mean (GPjax_p.predict, models.py:456-462) with

@@ -152,7 +152,7 @@ __device__ __forceinline__ double knn_dist_row(const double *__restrict__ X, int
     double acc = 0.0;
     int c = 0;
     if ((((uintptr_t)xr | (uintptr_t)q) & 15) == 0) {   // 16-byte aligned rows: double2 loads
-        constexpr int B = 16;                            // 16 loads in flight per lane
+        constexpr int B = 32;                            // 32 loads in flight per lane
         for (; c + 2 * B <= d; c += 2 * B) {
             double2 v[B];
 #pragma unroll
@@ -266,9 +266,14 @@ static inline int knn_xs_doubles(int m, int64_t d) { return (int64_t)m * (d + 1)
 static inline size_t knn_xs_bytes(int m, int64_t d) { return (size_t)knn_xs_doubles(m, d) * sizeof(double); }
 
 // LDS of one select (the caller's: a kernel-level __shared__ object, one per kernel)
+static constexpr int SEL_CAND = 256;   // candidates the threshold select ranks exactly
 struct SelShm {
     int32_t sel[64];
     double seld[64];
+    uint32_t hist[256];
+    uint64_t ck[SEL_CAND];
+    int ci[SEL_CAND];
+    int nc, digit, need;
     uint64_t rk[16][64];   // m <= 64
     int ri[16][64];
     uint64_t wk[4][64];
@@ -297,6 +302,40 @@ static void launch_knn_select(dim3 grid, size_t shmem, hipStream_t st, const dou
         hipLaunchKernelGGL(knn_select_kernel<0>, grid, dim3(256), shmem, st, dist, rows, args...);
 }
 
+// pw_leaf (8 <= n <= 128) on the 8 lanes of an aligned octet, lane j = lane & 7: lane j sums the
+// elements i = j (mod 8) below n - n%8 in ascending order (pw_leaf's r[j]); the octet combines
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) with DPP moves (lane^1, lane^2, then the mirrored 4-block;
+// a+b == b+a, so every lane holds the same bits); the n%8 tail follows in ascending order.
+// Bitwise pw_leaf, with 8 lanes on one pair instead of one.  All 8 lanes must be active.
+__device__ __forceinline__ double pw_leaf_octet(const double *__restrict__ a, const double *__restrict__ b, int n,
+                                                int j) {
+    const int nb = n - (n % 8);
+    double av[16], bv[16];   // all loads in flight before the sum (n <= 128: <= 16 per lane)
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+        const int i = j + 8 * u;
+        av[u] = i < nb ? a[i] : 0.0;
+        bv[u] = i < nb ? b[i] : 0.0;
+    }
+    double t = av[0] - bv[0];
+    double r = t * t;
+#pragma unroll
+    for (int u = 1; u < 16; u++) {
+        if (8 * u < nb) {   // nb is a multiple of 8: the same trip count on every lane
+            t = av[u] - bv[u];
+            r += t * t;
+        }
+    }
+    r = r + __builtin_amdgcn_mov_dpp(r, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+    r = r + __builtin_amdgcn_mov_dpp(r, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+    r = r + __builtin_amdgcn_mov_dpp(r, 0x141, 0xF, 0xF, false);   // row_half_mirror
+    for (int i = nb; i < n; i++) {
+        t = a[i] - b[i];
+        r += t * t;
+    }
+    return r;
+}
+
 // one workgroup of 256 threads per query (blockIdx.y; batched outputs at query-strided offsets).
 // spec_idx / hit_flag (single query): hit_flag = 1 iff the selected ordered neighbour list equals
 // spec_idx, else 2 iff it equals spec2_idx (when given), else 0 -- the speculative sweep then
@@ -307,7 +346,10 @@ __device__ __forceinline__ void knn_select_dev(
     const double *__restrict__ Y, int d, const double *__restrict__ q, int32_t *__restrict__ idx_out,
     double *__restrict__ dist_out, double *__restrict__ ymT, double *__restrict__ D2,
     double *__restrict__ kd2, const int32_t *__restrict__ spec_idx, int32_t *__restrict__ hit_flag,
-    int xs_doubles, const int32_t *__restrict__ spec2_idx, int32_t *host_flag) {
+    int xs_doubles, const int32_t *__restrict__ spec2_idx, int32_t *host_flag, uint64_t *marks = nullptr) {
+    // marks (profiling, thread 0's clock): after the rounds | the merges | the gathers | D2
+#define SEL_MARK(k) \
+    if (marks && tid == 0) marks[k] += wall_clock64();
     int32_t *sel = sh.sel;
     double *seld = sh.seld;
     uint64_t(*rk)[64] = sh.rk;
@@ -315,60 +357,171 @@ __device__ __forceinline__ void knn_select_dev(
     uint64_t(*wk)[64] = sh.wk;
     int(*wi)[64] = sh.wi;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // K > 0: the thread's K keys (rows tid + 256*j) stay in registers
+    uint64_t kv[K > 0 ? K : 1];
+    int kr[K > 0 ? K : 1];
+    if constexpr (K > 0) {
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            const int r = tid + 256 * j;
+            kr[j] = r < rows ? r : -1;
+            kv[j] = r < rows ? dist_key(dist[r]) : 0;
+        }
+    }
+    // 0) threshold select (K > 0): the m-th smallest high word T of the keys by a 4-pass radix
+    //    select (8-bit digits, LDS histograms), then every row with high word <= T -- a superset
+    //    of the m nearest, usually m plus a few -- is ranked exactly by (key, row) against the
+    //    others.  Bitwise the rounds below (the ordered m smallest pairs are unique); they remain
+    //    the path when more than SEL_CAND rows tie at or below T (duplicated training rows).
+    bool done = false;
+    if constexpr (K > 0) {
+        uint32_t prefix = 0;
+        int need = m;
+        for (int pass = 0; pass < 4; pass++) {
+            const int shift = 24 - 8 * pass;
+            sh.hist[tid] = 0;   // 256 threads = 256 bins
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < K; j++) {
+                const uint32_t hk = (uint32_t)(kv[j] >> 32);
+                const bool in = kr[j] >= 0 && (pass == 0 || (hk >> (shift + 8)) == (prefix >> (shift + 8)));
+                if (in) atomicAdd(&sh.hist[(hk >> shift) & 255], 1u);
+            }
+            __syncthreads();
+            if (wid == 0) {   // the digit whose bin holds the need-th smallest: lane l scans bins 4l..4l+3
+                const uint32_t h0 = sh.hist[4 * lane], h1 = sh.hist[4 * lane + 1], h2 = sh.hist[4 * lane + 2],
+                               h3 = sh.hist[4 * lane + 3];
+                const int own = (int)(h0 + h1 + h2 + h3);
+                int incl = own;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int v = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += v;
+                }
+                const int excl = incl - own;
+                if (excl < need && need <= incl) {
+                    int c = excl, b = 0;
+                    const int hb[4] = {(int)h0, (int)h1, (int)h2, (int)h3};
+#pragma unroll
+                    for (int u = 0; u < 3; u++)
+                        if (b == u && c + hb[u] < need) {
+                            c += hb[u];
+                            b = u + 1;
+                        }
+                    sh.digit = 4 * lane + b;
+                    sh.need = need - c;
+                }
+            }
+            __syncthreads();
+            prefix |= (uint32_t)sh.digit << shift;
+            need = sh.need;
+        }
+        if (tid == 0) sh.nc = 0;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < K; j++)
+            if (kr[j] >= 0 && (uint32_t)(kv[j] >> 32) <= prefix) {
+                const int p = atomicAdd(&sh.nc, 1);
+                if (p < SEL_CAND) {
+                    sh.ck[p] = kv[j];
+                    sh.ci[p] = kr[j];
+                }
+            }
+        __syncthreads();
+        const int L = sh.nc;
+        if (L <= SEL_CAND) {   // uniform
+            for (int t = tid; t < L; t += 256) {
+                const uint64_t k0 = sh.ck[t];
+                const int i0 = sh.ci[t];
+                int rank = 0;
+#pragma unroll 8
+                for (int u = 0; u < L; u++) rank += key_less(sh.ck[u], sh.ci[u], k0, i0);
+                if (rank < m) {
+                    sel[rank] = i0;
+                    seld[rank] = __longlong_as_double((long long)k0);
+                }
+            }
+            done = true;
+        }
+    }
     // 1) each 16-lane row of the workgroup: its m best (key, index) pairs among its lanes' rows
     //    (row r of the training set belongs to thread r % 256), in ascending order, by m rounds of
     //    "smallest pair strictly after the previous pick" with a 4-level DPP row minimum
-    {
+    if (!done) {
         const int grp = tid >> 4;
-        // K > 0: the thread's K keys (rows tid + 256*j) stay in registers for all m rounds
-        uint64_t kv[K > 0 ? K : 1];
-        int kr[K > 0 ? K : 1];
         if constexpr (K > 0) {
+            // sort the thread's K pairs once (odd-even transposition; an empty slot, row -1, sorts
+            // last), then every round only the lanes' heads compete: the 16-lane minimum is the
+            // row's next pick and its owner pops its head (~3x fewer instructions per round than
+            // rescanning all K keys against the previous pick)
 #pragma unroll
-            for (int j = 0; j < K; j++) {
-                const int r = tid + 256 * j;
-                kr[j] = r < rows ? r : -1;
-                kv[j] = r < rows ? dist_key(dist[r]) : 0;
+            for (int p = 0; p < K; p++) {
+#pragma unroll
+                for (int j = p & 1; j + 1 < K; j += 2) {
+                    const bool sw = (kr[j + 1] >= 0) & ((kr[j] < 0) | key_less(kv[j + 1], kr[j + 1], kv[j], kr[j]));
+                    const uint64_t tk = kv[j];
+                    const int ti = kr[j];
+                    kv[j] = sw ? kv[j + 1] : kv[j];
+                    kr[j] = sw ? kr[j + 1] : kr[j];
+                    kv[j + 1] = sw ? tk : kv[j + 1];
+                    kr[j + 1] = sw ? ti : kr[j + 1];
+                }
             }
-        }
-        uint64_t pk = 0;   // (0, -1) precedes every (key, row >= 0)
-        int pi = -1;
-        for (int k = 0; k < m; k++) {
-            uint64_t bk = 0;
-            int bi = -1;
-            if constexpr (K > 0) {
+            for (int k = 0; k < m; k++) {
+                uint64_t bk = kv[0];
+                int bi = kr[0];
+                row_key_min(bk, bi);
+                if ((tid & 15) == 0) {
+                    rk[grp][k] = bk;
+                    ri[grp][k] = bi;
+                }
+                const bool pop = (bi >= 0) & (kr[0] == bi);   // rows are distinct: one owner
 #pragma unroll
-                for (int j = 0; j < K; j++)
-                    key_take(bk, bi, kv[j], key_less(pk, pi, kv[j], kr[j]) ? kr[j] : -1);
-            } else {
+                for (int j = 0; j + 1 < K; j++) {
+                    kv[j] = pop ? kv[j + 1] : kv[j];
+                    kr[j] = pop ? kr[j + 1] : kr[j];
+                }
+                kv[K - 1] = pop ? 0 : kv[K - 1];
+                kr[K - 1] = pop ? -1 : kr[K - 1];
+            }
+        } else {
+            uint64_t pk = 0;   // (0, -1) precedes every (key, row >= 0)
+            int pi = -1;
+            for (int k = 0; k < m; k++) {
+                uint64_t bk = 0;
+                int bi = -1;
                 for (int r = tid; r < rows; r += 256) {
                     const uint64_t v = dist_key(dist[r]);
                     key_take(bk, bi, v, key_less(pk, pi, v, r) ? r : -1);
                 }
-            }
-            row_key_min(bk, bi);
-            if ((tid & 15) == 0) {
-                rk[grp][k] = bk;
-                ri[grp][k] = bi;
-            }
-            if (bi >= 0) {   // an exhausted row keeps its last pick (no re-picking from the start)
-                pk = bk;
-                pi = bi;
+                row_key_min(bk, bi);
+                if ((tid & 15) == 0) {
+                    rk[grp][k] = bk;
+                    ri[grp][k] = bi;
+                }
+                if (bi >= 0) {   // an exhausted row keeps its last pick (no re-picking from the start)
+                    pk = bk;
+                    pi = bi;
+                }
             }
         }
     }
     __syncthreads();
+    SEL_MARK(0);
     // 2) each wave merges its 4 row lists by rank (a pair's rank = how many valid pairs precede
     //    it; pairs are distinct, so ranks are too), 3) wave 0 merges the 4 wave lists the same way
-    for (int t = lane; t < m; t += 64) wi[wid][t] = -1;
-    rank_merge(&rk[4 * wid], &ri[4 * wid], m, lane, wk[wid], wi[wid]);
-    __syncthreads();
-    if (wid == 0) rank_merge(wk, wi, m, lane, (uint64_t *)nullptr, sel, seld);
-    __syncthreads();
+    if (!done) {   // uniform
+        for (int t = lane; t < m; t += 64) wi[wid][t] = -1;
+        rank_merge(&rk[4 * wid], &ri[4 * wid], m, lane, wk[wid], wi[wid]);
+        __syncthreads();
+        if (wid == 0) rank_merge(wk, wi, m, lane, (uint64_t *)nullptr, sel, seld);
+        __syncthreads();
+    }
     for (int k = tid; k < m; k += 256) {
         idx_out[k] = sel[k];
         if (dist_out) dist_out[k] = seld[k];
     }
+    SEL_MARK(1);
     if (hit_flag && wid == 0) {   // lane k compares entry k of the lists: one round trip, not m
         bool ne1 = false, ne2 = spec2_idx == nullptr;
         for (int k = lane; k < m; k += 64) {
@@ -424,9 +577,38 @@ __device__ __forceinline__ void knn_select_dev(
                 }
             }
         __syncthreads();
-        // the pairs, then kd2 on the next threads (one pass for m <= 21)
+        SEL_MARK(2);
+        // the pairs, then kd2 on the next tasks
         const int npairs = m * (m + 1) / 2;
-        for (int t = tid; t < npairs + (kd2 ? m : 0); t += 256) {
+        const int ntask = npairs + (kd2 ? m : 0);
+        if (staged && d >= 8 && d <= 128) {   // an octet of lanes per pair (pw_leaf_octet)
+            const int j8 = tid & 7;
+            const int nrnd = (ntask + 31) / 32;   // whole octets iterate together
+            for (int rd = 0; rd < nrnd; rd++) {
+                const int t = rd * 32 + (tid >> 3);
+                const bool valid = t < ntask;
+                const bool is_kd = valid && t >= npairs;
+                int r = 0, jj = 0;
+                if (valid && !is_kd) {
+                    while ((r + 1) * (r + 2) / 2 <= t) r++;
+                    jj = t - r * (r + 1) / 2;
+                } else if (is_kd) {
+                    r = t - npairs;
+                }
+                const double *xr = xs + (size_t)r * ds;
+                const double *xj = is_kd ? q : xs + (size_t)jj * ds;
+                const double v = pw_leaf_octet(xr, xj, d, j8);
+                if (valid && j8 == 0) {
+                    if (is_kd) {
+                        kd2[r] = v;
+                    } else {
+                        D2[r * m + jj] = v;
+                        D2[jj * m + r] = v;
+                    }
+                }
+            }
+        } else
+        for (int t = tid; t < ntask; t += 256) {
             if (t >= npairs) {
                 const int r = t - npairs;
                 kd2[r] = pw_sqdiff(staged ? xs + (size_t)r * ds : X + (int64_t)sel[r] * d, q, d);
@@ -442,6 +624,9 @@ __device__ __forceinline__ void knn_select_dev(
             D2[j * m + r] = v;
         }
     }
+    __syncthreads();
+    SEL_MARK(3);
+#undef SEL_MARK
 }
 
 template <int K>
@@ -1427,7 +1612,7 @@ __global__ void __launch_bounds__(256) chain_kernel(ChainArgs c) {
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
     const int d = c.a.d, m = c.a.m;
     uint32_t target = 0;
-    uint64_t g_ticks = 0, pt[4] = {0, 0, 0, 0}, tp = 0;
+    uint64_t g_ticks = 0, pt[4] = {0, 0, 0, 0}, tp = 0, sm4[4] = {0, 0, 0, 0}, cyc = 0;
     const bool prof = c.prof != nullptr && blockIdx.x == 0;
 #define CHAIN_MARK(k)                          \
     if (prof) {                                \
@@ -1468,6 +1653,11 @@ __global__ void __launch_bounds__(256) chain_kernel(ChainArgs c) {
         CHAIN_MARK(1);
         // 3) ordered neighbour list, y_m, D2, kd2 and the hit code
         if (blockIdx.x == 0) {
+            if (prof && tid == 0) {   // select sub-phases relative to its start
+                const uint64_t now = wall_clock64();
+                for (int k = 0; k < 4; k++) sm4[k] -= now;
+                cyc -= clock64();
+            }
             const int32_t *s2 = c.spec2_idx ? c.spec2_idx + j * m : nullptr;
             const int32_t *s1 = c.spec_idx + j * m;
             int32_t *fl = c.flags + j;
@@ -1475,17 +1665,18 @@ __global__ void __launch_bounds__(256) chain_kernel(ChainArgs c) {
             double *D2 = const_cast<double *>(c.a.D2), *kd2 = const_cast<double *>(c.a.kd2);
             switch (c.kk) {
             case 2: knn_select_dev<2>(sh, c.dist, c.rows, m, c.X, c.Yd, d, qs, c.idx, nullptr, ymT, D2, kd2, s1, fl,
-                                      c.xs_doubles, s2, nullptr); break;
+                                      c.xs_doubles, s2, nullptr, prof ? sm4 : nullptr); break;
             case 4: knn_select_dev<4>(sh, c.dist, c.rows, m, c.X, c.Yd, d, qs, c.idx, nullptr, ymT, D2, kd2, s1, fl,
-                                      c.xs_doubles, s2, nullptr); break;
+                                      c.xs_doubles, s2, nullptr, prof ? sm4 : nullptr); break;
             case 8: knn_select_dev<8>(sh, c.dist, c.rows, m, c.X, c.Yd, d, qs, c.idx, nullptr, ymT, D2, kd2, s1, fl,
-                                      c.xs_doubles, s2, nullptr); break;
+                                      c.xs_doubles, s2, nullptr, prof ? sm4 : nullptr); break;
             case 16: knn_select_dev<16>(sh, c.dist, c.rows, m, c.X, c.Yd, d, qs, c.idx, nullptr, ymT, D2, kd2, s1,
-                                        fl, c.xs_doubles, s2, nullptr); break;
+                                        fl, c.xs_doubles, s2, nullptr, prof ? sm4 : nullptr); break;
             default: knn_select_dev<0>(sh, c.dist, c.rows, m, c.X, c.Yd, d, qs, c.idx, nullptr, ymT, D2, kd2, s1,
-                                       fl, c.xs_doubles, s2, nullptr); break;
+                                       fl, c.xs_doubles, s2, nullptr, prof ? sm4 : nullptr); break;
             }
         }
+        if (prof && tid == 0) cyc += clock64();
         chain_barrier(c.bar, target);
         CHAIN_MARK(2);
         const int hit = __hip_atomic_load(c.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1508,7 +1699,11 @@ __global__ void __launch_bounds__(256) chain_kernel(ChainArgs c) {
     }
 #undef CHAIN_MARK
     if (prof && tid == 0)
-        for (int k = 0; k < 4; k++) __hip_atomic_store(c.prof + k, pt[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int k = 0; k < 4; k++) {
+            __hip_atomic_store(c.prof + k, pt[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(c.prof + 4 + k, sm4[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(c.prof + 8, cyc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     if (blockIdx.x == 0 && tid == 0) {
         __hip_atomic_store(c.g_ticks, g_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(c.stop, i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1936,7 +2131,7 @@ static int chain_resources(ChainRes **out) {
         NNGP_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
         r.tick_khz = khz > 0 ? khz : 100000.0;
         NNGP_HIP_CHECK(hipMalloc((void **)&r.bar, 256));
-        NNGP_HIP_CHECK(hipHostMalloc((void **)&r.stop, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        NNGP_HIP_CHECK(hipHostMalloc((void **)&r.stop, 128, hipHostMallocMapped | hipHostMallocCoherent));
         r.dev = dev;
     }
     *out = &r;
@@ -1945,10 +2140,11 @@ static int chain_resources(ChainRes **out) {
 
 // the systems / shapes the chain's in-kernel G covers (the rest keep the launch chain):
 // every ODE (lane form) and Burgers with d = 64*EPT <= 256 (wave form); exact G, m <= 32.
-// NNGP_CHAIN=0 disables it (A/B).
+// Opt-in (NNGP_CHAIN=1): measured on the box it is bitwise the launch chain but not faster --
+// 0.90-1.00x on Lorenz / FHN-ODE / Hopf / Burgers (tools/chain_probe.py).
 bool chain_supported(const nngp_system *sys, int g_step_mode, int m) {
     const char *e = getenv("NNGP_CHAIN");
-    if (e && atoi(e) == 0) return false;
+    if (!e || atoi(e) == 0) return false;
     if (g_step_mode & NNGP_STEP_CONTRACT) return false;
     if (m < 1 || m > 32 || sys->d > CHAIN_QMAX) return false;
     switch (sys->kind) {
@@ -2039,7 +2235,10 @@ int chain_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t 
     const size_t lds = std::max(knn_xs_bytes(m, d),
                                 sizeof(double) * ((size_t)m * m + m + 16 * k_image_doubles(maxm)));
     NNGP_REQUIRE(lds + sizeof(SelShm) + sizeof(double) * CHAIN_QMAX <= 160 * 1024, "chain: LDS");
-    const int nb = std::max(1, std::min(c.n_mean_blk, 64));
+    // workgroups: one per 16 coordinates of the mean phase (NNGP_CHAIN_WGS overrides; 1 = no grid
+    // barrier at all)
+    static const int wgs_env = getenv("NNGP_CHAIN_WGS") ? atoi(getenv("NNGP_CHAIN_WGS")) : 0;
+    const int nb = std::max(1, std::min(wgs_env > 0 ? wgs_env : c.n_mean_blk, 64));
     res->stop[0] = -1;
     NNGP_HIP_CHECK(hipMemsetAsync(res->bar, 0, sizeof(uint32_t), st));
     switch (maxm) {
@@ -2059,9 +2258,13 @@ int chain_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t 
     *stop_out = stop;
     if (g_ms_out) *g_ms_out += (float)((double)*c.g_ticks / res->tick_khz);
     if (c.prof)
-        fprintf(stderr, "chain i0=%d stop=%d d=%d rows=%lld nb=%d us: G %.1f kNN %.1f select %.1f mean %.1f\n", i0,
-                stop, d, (long long)rows, nb, c.prof[0] / res->tick_khz * 1e3, c.prof[1] / res->tick_khz * 1e3,
-                c.prof[2] / res->tick_khz * 1e3, c.prof[3] / res->tick_khz * 1e3);
+        fprintf(stderr,
+                "chain i0=%d stop=%d d=%d rows=%lld nb=%d us: G %.1f kNN %.1f select %.1f mean %.1f"
+                " | select marks %.1f %.1f %.1f %.1f | select shader cycles %.0f\n",
+                i0, stop, d, (long long)rows, nb, c.prof[0] / res->tick_khz * 1e3, c.prof[1] / res->tick_khz * 1e3,
+                c.prof[2] / res->tick_khz * 1e3, c.prof[3] / res->tick_khz * 1e3, (double)(int64_t)c.prof[4] / res->tick_khz * 1e3,
+                (double)(int64_t)c.prof[5] / res->tick_khz * 1e3, (double)(int64_t)c.prof[6] / res->tick_khz * 1e3,
+                (double)(int64_t)c.prof[7] / res->tick_khz * 1e3, (double)c.prof[8]);
     {
         std::lock_guard<std::mutex> lk(g_chain_mu);
         g_chain_launches++;
