@@ -100,9 +100,11 @@ __device__ double pw_leaf(const double *__restrict__ a, const double *__restrict
     return res;
 }
 
-__device__ double pw_sqdiff(const double *__restrict__ a, const double *__restrict__ b, int n) {
-    if (n <= 128) return pw_leaf(a, b, n);
-    // post-order walk of numpy's recursion: split at n2 = n/2 - (n/2)%8 until n <= 128
+// numpy's pairwise recursion over n terms (split at n2 = n/2 - (n/2)%8 until n <= 128) as a
+// post-order walk: leaf(off, len) gives a leaf's value, the walk combines them as the recursion does
+template <typename Leaf>
+__device__ __forceinline__ double pw_walk(int n, Leaf &&leaf) {
+    if (n <= 128) return leaf(0, n);
     int off[32], len[32], stage[32];
     double left[32];
     int sp = 1;
@@ -126,7 +128,7 @@ __device__ double pw_sqdiff(const double *__restrict__ a, const double *__restri
             continue;
         }
         if (len[t] <= 128) {
-            ret = pw_leaf(a + off[t], b + off[t], len[t]);
+            ret = leaf(off[t], len[t]);
             have = true;
             sp--;
             continue;
@@ -137,6 +139,10 @@ __device__ double pw_sqdiff(const double *__restrict__ a, const double *__restri
         off[sp] = off[t]; len[sp] = n2; stage[sp] = 0; sp++;
     }
     return ret;
+}
+
+__device__ double pw_sqdiff(const double *__restrict__ a, const double *__restrict__ b, int n) {
+    return pw_walk(n, [&](int o, int l) { return pw_leaf(a + o, b + o, l); });
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -264,6 +270,12 @@ __device__ __forceinline__ void rank_merge(const uint64_t (*k)[64], const int (*
 // LDS staging of the m selected rows for the pair distances (at most 48 KB; larger m*d reads X)
 static inline int knn_xs_doubles(int m, int64_t d) { return (int64_t)m * (d + 1) <= 6144 ? (int)(m * (d + 1)) : 0; }
 static inline size_t knn_xs_bytes(int m, int64_t d) { return (size_t)knn_xs_doubles(m, d) * sizeof(double); }
+// D2/kd2 by d2_wave_kernel (a wave per pair) where the select's own pass would leave one lane per
+// pair walking d terms from global memory: d > 128 or rows not staged.  NNGP_D2_WAVES=0: never.
+static inline bool d2_by_waves(int m, int d) {
+    static const int env = getenv("NNGP_D2_WAVES") ? atoi(getenv("NNGP_D2_WAVES")) : 1;
+    return env != 0 && (d > 128 || knn_xs_doubles(m, d) == 0);
+}
 
 // LDS of one select (the caller's: a kernel-level __shared__ object, one per kernel)
 static constexpr int SEL_CAND = 256;   // candidates the threshold select ranks exactly
@@ -647,6 +659,69 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
     if (kd2) kd2 += (size_t)qy * m;
     knn_select_dev<K>(sh, dist, rows, m, X, Y, d, q, idx_out, dist_out, ymT, D2, kd2, spec_idx, hit_flag,
                       xs_doubles, spec2_idx, host_flag);
+}
+
+// D2 / kd2 of the m selected rows when d > 128 or the rows do not fit the select's LDS staging:
+// ONE WAVE per pair (blockIdx.x < m(m+1)/2) or per kd2 row (the next m blocks), query blockIdx.y.
+// The pair's numpy leaves (pw_walk) go to the wave's 8 octets (pw_leaf_octet; a leaf is >= 64
+// terms here), their values to LDS, and lane 0 combines them in the recursion's order: bitwise
+// pw_sqdiff, with 64 lanes and all loads in flight instead of one lane walking d terms
+// (FHN-PDE d = 800, m = 20: 230 such sums per prediction).
+__global__ void __launch_bounds__(64) d2_wave_kernel(const double *__restrict__ X, const int32_t *__restrict__ idx,
+                                                     int m, int d, const double *__restrict__ q,
+                                                     double *__restrict__ D2, double *__restrict__ kd2) {
+    __shared__ double leafv[16];
+    __shared__ int leafo[16], leafl[16];
+    __shared__ int nleaf;
+    const int qy = blockIdx.y;
+    idx += (size_t)qy * m;
+    q += (size_t)qy * d;
+    D2 += (size_t)qy * m * m;
+    if (kd2) kd2 += (size_t)qy * m;
+    const int t = blockIdx.x, lane = threadIdx.x;
+    const int npairs = m * (m + 1) / 2;
+    int r = 0, j = 0;
+    const bool is_kd = t >= npairs;
+    if (!is_kd) {
+        while ((r + 1) * (r + 2) / 2 <= t) r++;
+        j = t - r * (r + 1) / 2;
+    } else {
+        r = t - npairs;
+    }
+    const double *a = X + (int64_t)idx[r] * d;
+    const double *b = is_kd ? q : X + (int64_t)idx[j] * d;
+    if (lane == 0) {   // the leaves, left to right
+        int k = 0;
+        pw_walk(d, [&](int o, int l) {
+            leafo[k] = o;
+            leafl[k] = l;
+            k++;
+            return 0.0;
+        });
+        nleaf = k;
+    }
+    __syncthreads();
+    const int nl = nleaf;
+    for (int base = 0; base < nl; base += 8) {   // octet o computes leaf base + o
+        const int lf = base + (lane >> 3);
+        const bool ok = lf < nl;
+        const int o = ok ? leafo[lf] : 0, l = ok ? leafl[lf] : 8;
+        double v;
+        if (l >= 8) v = pw_leaf_octet(a + o, b + o, l, lane & 7);
+        else v = pw_leaf(a + o, b + o, l);   // (d < 8: one leaf)
+        if (ok && (lane & 7) == 0) leafv[lf] = v;
+    }
+    __syncthreads();
+    if (lane == 0) {
+        int k = 0;
+        const double v = pw_walk(d, [&](int, int) { return leafv[k++]; });
+        if (is_kd) {
+            kd2[r] = v;
+        } else {
+            D2[r * m + j] = v;
+            D2[j * m + r] = v;
+        }
+    }
 }
 
 // D2 / kd2 from an explicit xm (unfused entry points)
@@ -2026,11 +2101,18 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
     hipLaunchKernelGGL(knn_dist_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, X, rows,
                        d, new_x, dist);
     NNGP_LAUNCH_CHECK();
+    const bool wave_d2 = d2_by_waves(m, d);
     launch_knn_select(dim3(1), knn_xs_bytes(m, d), st, dist, rows, m, X, Y, d, new_x, idx, (double *)nullptr,
-                      ymT, D2, kd2, spec ? spec_idx : (const int32_t *)nullptr,
+                      ymT, wave_d2 ? (double *)nullptr : D2, wave_d2 ? (double *)nullptr : kd2,
+                      spec ? spec_idx : (const int32_t *)nullptr,
                       spec ? hit_flag : (int32_t *)nullptr, knn_xs_doubles(m, d),
                       spec ? spec2_idx : (const int32_t *)nullptr, spec ? host_flag : (int32_t *)nullptr);
     NNGP_LAUNCH_CHECK();
+    if (wave_d2) {
+        hipLaunchKernelGGL(d2_wave_kernel, dim3((unsigned)(m * (m + 1) / 2 + m)), dim3(64), 0, st, X, idx, m, d,
+                           new_x, D2, kd2);
+        NNGP_LAUNCH_CHECK();
+    }
     // coordinates [c0, c1) only (the multi-rank sweep's share): the fits and means of those
     // columns, in the same product(coord, jitter, restart) order with their own theta0 draws
     const int dc = c1 - c0;
@@ -2090,10 +2172,17 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
     hipLaunchKernelGGL(knn_dist_kernel, dim3((unsigned)((rows + 63) / 64), (unsigned)nq), dim3(64), 0, st, X,
                        rows, d, Q, dist);
     NNGP_LAUNCH_CHECK();
+    const bool wave_d2 = d2_by_waves(m, d);
     launch_knn_select(dim3(1, (unsigned)nq), knn_xs_bytes(m, d), st, dist, rows, m, X, Y, d, Q, idx_out,
-                      (double *)nullptr, ymT, D2, (double *)nullptr, (const int32_t *)nullptr,
-                      (int32_t *)nullptr, knn_xs_doubles(m, d), (const int32_t *)nullptr, (int32_t *)nullptr);
+                      (double *)nullptr, ymT, wave_d2 ? (double *)nullptr : D2, (double *)nullptr,
+                      (const int32_t *)nullptr, (int32_t *)nullptr, knn_xs_doubles(m, d), (const int32_t *)nullptr,
+                      (int32_t *)nullptr);
     NNGP_LAUNCH_CHECK();
+    if (wave_d2) {
+        hipLaunchKernelGGL(d2_wave_kernel, dim3((unsigned)(m * (m + 1) / 2), (unsigned)nq), dim3(64), 0, st, X,
+                           idx_out, m, d, Q, D2, (double *)nullptr);
+        NNGP_LAUNCH_CHECK();
+    }
     a.m = m; a.d = d; a.n_fits = (int)nfp;
     a.D2 = D2; a.Y = ymT; a.ys_c = m; a.ys_r = 1;
     a.theta0 = theta0; a.fatol = fatol; a.xatol = xatol; a.maxfev = maxfev; a.R = n_restarts;
