@@ -1169,9 +1169,17 @@ __device__ __forceinline__ double jit_lookup(const NMArgs &a, int j) {
 template <int MAXM> struct NMBound { static constexpr int T = (MAXM <= 16) ? 512 : (MAXM <= 32 ? 256 : 64); };
 // threads of the wave-per-fit speculative kernel and of the mean kernel
 template <int MAXM> struct WGT { static constexpr int T = MAXM > 32 ? 64 : 256; };
+// minimum waves per SIMD the fits kernels are register-allocated for (NNGP_NM_WAVES at build time;
+// 1 = no constraint).  MAXM <= 16 takes ~180 VGPRs (2 waves); -DNNGP_NM_WAVES=3 caps them at 168
+// with 84-108 bytes of spills: measured slower (Burgers N=128 0.305 -> 0.314-0.321 s, d=128
+// correction 0.626 -> 0.702 ms), so not kept
+#ifndef NNGP_NM_WAVES
+#define NNGP_NM_WAVES 1
+#endif
+template <int MAXM> struct NMWaves { static constexpr int W = MAXM <= 16 ? NNGP_NM_WAVES : 1; };
 
 template <int MAXM, bool FUSED>
-__global__ void __launch_bounds__(NMBound<MAXM>::T) nm_fit_kernel(NMArgs a) {
+__global__ void __launch_bounds__(NMBound<MAXM>::T, NMWaves<MAXM>::W) nm_fit_kernel(NMArgs a) {
     constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG;
     extern __shared__ __attribute__((aligned(16))) double sm[];
     if (a.skip && *a.skip) return;   // uniform: the whole grid exits
@@ -1367,7 +1375,7 @@ __device__ __forceinline__ int nm_candidates(const NM &S, NMCand (&c)[4]) {
 }
 
 template <int MAXM>
-__global__ void __launch_bounds__(WGT<MAXM>::T) nm_spec_kernel(NMArgs a) {
+__global__ void __launch_bounds__(WGT<MAXM>::T, NMWaves<MAXM>::W) nm_spec_kernel(NMArgs a) {
     constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG;
     extern __shared__ __attribute__((aligned(16))) double sm[];
     if (a.skip && *a.skip) return;   // uniform: the whole grid exits (speculation hit)
