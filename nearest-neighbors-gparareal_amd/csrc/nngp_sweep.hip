@@ -41,13 +41,14 @@ struct Respec {
     int dev = -1;
     hipStream_t st2 = nullptr;
     hipEvent_t ev_g = nullptr, ev_r = nullptr;
+    std::vector<hipEvent_t> ev_q;   // per query of the window (split re-speculation)
     int32_t *hflags = nullptr;   // host-mapped, fine-grained
     size_t nflags = 0;
 };
 static Respec g_respec;
 static std::mutex g_respec_mu;
 
-static int respec_resources(size_t nflags, Respec **out) {
+static int respec_resources(size_t nflags, int w, Respec **out) {
     std::lock_guard<std::mutex> lk(g_respec_mu);
     Respec &r = g_respec;
     int dev = 0;
@@ -56,6 +57,7 @@ static int respec_resources(size_t nflags, Respec **out) {
         if (r.st2) (void)hipStreamDestroy(r.st2);
         if (r.ev_g) (void)hipEventDestroy(r.ev_g);
         if (r.ev_r) (void)hipEventDestroy(r.ev_r);
+        for (hipEvent_t e : r.ev_q) (void)hipEventDestroy(e);
         if (r.hflags) (void)hipHostFree(r.hflags);
         r = Respec{};
         int lo = 0, hi = 0;
@@ -66,6 +68,11 @@ static int respec_resources(size_t nflags, Respec **out) {
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_g, hipEventDisableTiming));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_r, hipEventDisableTiming));
         r.dev = dev;
+    }
+    while ((int)r.ev_q.size() < w) {
+        hipEvent_t e;
+        NNGP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        r.ev_q.push_back(e);
     }
     if (r.nflags < nflags) {
         if (r.hflags) (void)hipHostFree(r.hflags);
@@ -170,7 +177,7 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
     const int W = spec ? (int)std::min<int64_t>(respec_window(), nq - 1) : 0;
     Respec *rs = nullptr;
     if (W > 0) {
-        const int rc0 = respec_resources((size_t)nq, &rs);
+        const int rc0 = respec_resources((size_t)nq, W, &rs);
         if (rc0) return rc0;
     }
     if (spec) {
@@ -212,6 +219,11 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
         if (rc) return rc;
     }
     bool respec_pending = false;
+    // NNGP_RESPEC_SPLIT (default 0): the window's re-speculation as one launch set per slice, each
+    // slice waiting for its own (launch chain only).  Measured slower (Burgers N=128 0.297 -> 0.413
+    // s): on one side stream the sets run one after another instead of as one parallel launch
+    const bool split = W > 0 && env_int("NNGP_RESPEC_SPLIT", 0) != 0;
+    std::vector<int> pend(split ? (size_t)nq : 0, -1);   // per slice: its window event, or -1
     // ---- the fused chain (nngp_gp.hip chain_kernel): runs of hit slices as one persistent kernel;
     // the host takes over at each miss (that slice's fits, the re-speculation), then resumes it
     const bool chained = spec && chain_supported(sys, g_step_mode, m);
@@ -278,8 +290,13 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
         }
         if (W > 0) {
             NNGP_HIP_CHECK(hipEventRecord(rs->ev_g, st));                  // G(U1[i]) done
-            if (respec_pending) NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_r, 0));   // lists/fits ready
-            respec_pending = false;
+            if (split) {   // this slice's re-speculated list/fits ready (not the whole window's)
+                if (pend[j] >= 0) NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_q[pend[j]], 0));
+                pend[j] = -1;
+            } else {
+                if (respec_pending) NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_r, 0));   // lists/fits ready
+                respec_pending = false;
+            }
         }
         rc = predict_impl(X, Y, rows, d, ui, m, n_jitter, jitter_exp_host, n_restarts, theta0 + j * n_fits * 2, fatol,
                           xatol, maxfev, preds_scratch, ug_next, u_next, nullptr, spec ? spec_idx + j * m : nullptr,
@@ -304,10 +321,24 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
                 rc = nngp_parareal_update(d, UF + (size_t)(s + 1) * d, UG + (size_t)(s + 1) * d, g2,
                                           Qr + (size_t)q * d, s2);
         }
-        if (rc == NNGP_OK)
+        if (rc == NNGP_OK && split) {
+            // one launch set per guessed slice, nearest first, each with its own event: slice i+1
+            // waits for its own fits only, not for the window's (they otherwise finish together,
+            // throughput-bound, behind this miss's own fits)
+            for (int q = 0; q < w && rc == NNGP_OK; q++) {
+                rc = spec_batch(X, Y, rows, d, Qr + (size_t)q * d, 1, m, n_jitter, jitter_exp_host, n_restarts,
+                                theta0 + (j + 1 + q) * n_fits * 2, fatol, xatol, maxfev, spec2_idx + (j + 1 + q) * m,
+                                spec2_fits + (j + 1 + q) * n_fits * 4, env_int("NNGP_RESPEC_PACKED", 0) == 0, s2);
+                if (rc == NNGP_OK) {
+                    NNGP_HIP_CHECK(hipEventRecord(rs->ev_q[q], s2));
+                    pend[j + 1 + q] = q;
+                }
+            }
+        } else if (rc == NNGP_OK) {
             rc = spec_batch(X, Y, rows, d, Qr, w, m, n_jitter, jitter_exp_host, n_restarts,
                             theta0 + (j + 1) * n_fits * 2, fatol, xatol, maxfev, spec2_idx + (j + 1) * m,
                             spec2_fits + (j + 1) * n_fits * 4, env_int("NNGP_RESPEC_PACKED", 0) == 0, s2);
+        }
         if (rc == NNGP_OK) {
             NNGP_HIP_CHECK(hipEventRecord(rs->ev_r, s2));
             respec_pending = true;
