@@ -48,7 +48,8 @@ void set_error(const char *fmt, ...);
 // speculative sweep's batch buffers, which must outlive the per-slice calls.  Growing a slot
 // frees the old buffer after hipFree's implicit device synchronisation.  Not thread-safe across
 // host threads sharing a device.
-constexpr int N_WS_SLOTS = 6;   // slot 2: the sweep's speculation buffers; 3: full-GP factors; 4: fit queues; 5: parked fits
+constexpr int N_WS_SLOTS = 7;   // slot 2: the sweep's speculation buffers; 3: full-GP factors; 4: fit queues; 5: parked fits;
+                                // 6: the re-speculation window's batch (slot 1 may still be read by an overlapped batch)
 void *workspace(size_t bytes, int *err, int slot = 0);
 
 int predict_impl(const double *X, const double *Y, int64_t rows, int d, const double *new_x, int m,
@@ -56,13 +57,14 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
                  double fatol, double xatol, int maxfev, double *preds_out, const double *bias,
                  double *out, double *fits_out, const int32_t *spec_idx, const double *spec_fits,
                  int32_t *hit_flag, const int32_t *spec2_idx, const double *spec2_fits, int32_t *host_flag,
-                 hipStream_t st, int c0 = 0, int c1 = -1);
+                 hipStream_t st, int c0 = 0, int c1 = -1, const int32_t *wait_done = nullptr,
+                 int32_t *wait_err = nullptr);
 int gpfull_mean(const double *X, int64_t rows, int d, const double *q, const double *coef, const double *alpha,
                 const double *bias, double *out, hipStream_t st);
 int spec_batch(const double *X, const double *Y, int64_t rows, int d, const double *Q, int nq, int m,
                int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
                double fatol, double xatol, int maxfev, int32_t *idx_out, double *fits_out, bool latency,
-               hipStream_t st);
+               hipStream_t st, int slot = 1, int32_t *done = nullptr, hipEvent_t ev_select = nullptr);
 // the fused correction chain (nngp_gp.hip): one persistent kernel per run of hit slices
 bool chain_supported(const nngp_system *sys, int g_step_mode, int m);
 int chain_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps, const double *t, int I,

@@ -1144,6 +1144,13 @@ struct NMArgs {
     int jmajor;
     NM *park;
     int32_t *park_list, *park_count;
+    // overlapped speculative batch: the fits kernel counts each prediction's finished fits
+    // (done[blockIdx.y], after a device-scope fence); the sweep's mean kernel, on a hit served by
+    // that batch, waits until wait_done reaches wait_n (bounded: *err = 1 past ~2 s)
+    int32_t *done;
+    const int32_t *wait_done;
+    int wait_n;
+    int32_t *err;
 };
 
 // apply the blockIdx.y prediction offsets of a batched launch (all zero otherwise)
@@ -1267,6 +1274,10 @@ __global__ void __launch_bounds__(NMBound<MAXM>::T, NMWaves<MAXM>::W) nm_fit_ker
                 a.fits_out[4 * f + 1] = St.s0y;
                 a.fits_out[4 * f + 2] = fval;
                 a.fits_out[4 * f + 3] = (double)St.fcalls;
+            }
+            if (!FUSED && a.done) {   // the fit is visible device-wide before it is counted
+                __threadfence();
+                __hip_atomic_fetch_add(a.done + blockIdx.y, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             if (FUSED) {
                 sRes[4 * g + 0] = St.s0x;
@@ -1490,6 +1501,20 @@ __device__ __forceinline__ void gp_mean_dev(const NMArgs &a, int blk, bool load_
     const int m = a.m, d = a.d;
     double *sD2 = sm, *skd2 = sm + m * m, *sK = skd2 + m;
     const int tid = threadIdx.x, g = tid / 16, l = tid % 16;
+    if (a.wait_done) {   // a hit served by the overlapped batch: wait for its fits of this query
+        if (tid == 0 && __hip_atomic_load(a.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+            uint32_t spin = 0;
+            while (__hip_atomic_load(a.wait_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.wait_n) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spin > (1u << 24)) {   // never a hang: report and go on
+                    __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+            }
+            __threadfence();
+        }
+        __syncthreads();
+    }
     if (load_lds) {
         for (int i = tid; i < m * m; i += blockDim.x) sD2[i] = a.D2[i];
         for (int i = tid; i < m; i += blockDim.x) skd2[i] = a.kd2[i];
@@ -2082,7 +2107,7 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
                  double fatol, double xatol, int maxfev, double *preds_out, const double *bias,
                  double *out, double *fits_out, const int32_t *spec_idx, const double *spec_fits,
                  int32_t *hit_flag, const int32_t *spec2_idx, const double *spec2_fits, int32_t *host_flag,
-                 hipStream_t st, int c0, int c1) {
+                 hipStream_t st, int c0, int c1, const int32_t *wait_done, int32_t *wait_err) {
     NNGP_REQUIRE(X && Y && new_x && theta0 && preds_out, "null array argument");
     if (c1 < 0) c1 = d;
     NNGP_REQUIRE(0 <= c0 && c0 < c1 && c1 <= d, "bad coordinate range [%d, %d) of d=%d", c0, c1, d);
@@ -2135,6 +2160,11 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
         a.skip = hit_flag;
         a.fits_alt = spec_fits;
         a.fits_alt2 = spec2_fits;
+        if (wait_done) {   // the batch's fits may still be running (overlapped sweep)
+            a.wait_done = wait_done;
+            a.wait_n = (int)n_fits;
+            a.err = wait_err;
+        }
     }
     if (use_spec(a.n_fits, a.m)) {   // fits (a wave each), then arg-min + mean (+ bias) per coordinate
         rc = run_nm_spec(a, st);
@@ -2164,7 +2194,7 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
 int spec_batch(const double *X, const double *Y, int64_t rows, int d, const double *Q, int nq, int m,
                int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
                double fatol, double xatol, int maxfev, int32_t *idx_out, double *fits_out, bool latency,
-               hipStream_t st) {
+               hipStream_t st, int slot, int32_t *done, hipEvent_t ev_select) {
     NNGP_REQUIRE(nq >= 1 && m >= 1 && m <= MAX_M && m <= rows, "bad speculative batch shape");
     NMArgs a{};
     int rc = fill_jitters(a, n_jitter, jitter_exp_host);
@@ -2173,7 +2203,7 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
     // slot-1 workspace: dist[nq][rows] | D2[nq][m*m] | ymT[nq][d*m]
     int err = 0;
     double *dist = (double *)workspace(sizeof(double) * (size_t)nq * ((size_t)rows + (size_t)m * m + (size_t)d * m),
-                                       &err, 1);
+                                       &err, slot);
     if (err) return err;
     double *D2 = dist + (size_t)nq * rows;
     double *ymT = D2 + (size_t)nq * m * m;
@@ -2191,12 +2221,15 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
                            idx_out, m, d, Q, D2, (double *)nullptr);
         NNGP_LAUNCH_CHECK();
     }
+    if (ev_select) NNGP_HIP_CHECK(hipEventRecord(ev_select, st));   // the lists are ready
+    if (done) NNGP_HIP_CHECK(hipMemsetAsync(done, 0, sizeof(int32_t) * (size_t)nq, st));
     a.m = m; a.d = d; a.n_fits = (int)nfp;
     a.D2 = D2; a.Y = ymT; a.ys_c = m; a.ys_r = 1;
     a.theta0 = theta0; a.fatol = fatol; a.xatol = xatol; a.maxfev = maxfev; a.R = n_restarts;
     a.fits_out = fits_out;
     a.qs_D2 = (int64_t)m * m; a.qs_Y = (int64_t)d * m; a.qs_th = (int64_t)nfp * 2; a.qs_fits = (int64_t)nfp * 4;
     a.jmajor = getenv("NNGP_NM_JMAJOR") ? atoi(getenv("NNGP_NM_JMAJOR")) : 1;   // (run_nm_parked; Burgers 0.328 -> 0.317 s)
+    a.done = done;
     // latency: a wave per fit (the re-speculation window the sweep waits on); else packed fits
     if (latency) return run_nm_spec(a, st, nq);
     return run_nm(a, false, st, nq);
@@ -2419,7 +2452,7 @@ extern "C" int nngp_predict(const double *X, const double *Y, int64_t rows, int 
                             void *stream) {
     return nngp::predict_impl(X, Y, rows, d, new_x, m, n_jitter, jitter_exp_host, n_restarts, theta0, fatol,
                               xatol, maxfev, preds_out, bias, out, fits_out, nullptr, nullptr, nullptr, nullptr,
-                              nullptr, nullptr, (hipStream_t)stream, 0, d);
+                              nullptr, nullptr, (hipStream_t)stream, 0, d, nullptr, nullptr);
 }
 
 extern "C" int nngp_predict_range(const double *X, const double *Y, int64_t rows, int d, const double *new_x,
@@ -2428,5 +2461,5 @@ extern "C" int nngp_predict_range(const double *X, const double *Y, int64_t rows
                                   double *preds_out, void *stream) {
     return nngp::predict_impl(X, Y, rows, d, new_x, m, n_jitter, jitter_exp_host, n_restarts, theta0, fatol,
                               xatol, maxfev, preds_out, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                              nullptr, nullptr, nullptr, (hipStream_t)stream, c0, c1);
+                              nullptr, nullptr, nullptr, (hipStream_t)stream, c0, c1, nullptr, nullptr);
 }

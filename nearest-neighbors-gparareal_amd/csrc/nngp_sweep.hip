@@ -42,6 +42,9 @@ struct Respec {
     hipStream_t st2 = nullptr;
     hipEvent_t ev_g = nullptr, ev_r = nullptr;
     std::vector<hipEvent_t> ev_q;   // per query of the window (split re-speculation)
+    hipStream_t st3 = nullptr;      // the overlapped speculative batch
+    hipEvent_t ev_pre = nullptr, ev_sel = nullptr, ev_b = nullptr;
+    int32_t *herr = nullptr;        // host-mapped: a mean kernel's wait timed out
     int32_t *hflags = nullptr;   // host-mapped, fine-grained
     size_t nflags = 0;
 };
@@ -58,6 +61,10 @@ static int respec_resources(size_t nflags, int w, Respec **out) {
         if (r.ev_g) (void)hipEventDestroy(r.ev_g);
         if (r.ev_r) (void)hipEventDestroy(r.ev_r);
         for (hipEvent_t e : r.ev_q) (void)hipEventDestroy(e);
+        if (r.st3) (void)hipStreamDestroy(r.st3);
+        for (hipEvent_t e : {r.ev_pre, r.ev_sel, r.ev_b})
+            if (e) (void)hipEventDestroy(e);
+        if (r.herr) (void)hipHostFree(r.herr);
         if (r.hflags) (void)hipHostFree(r.hflags);
         r = Respec{};
         int lo = 0, hi = 0;
@@ -67,6 +74,11 @@ static int respec_resources(size_t nflags, int w, Respec **out) {
                                                    env_int("NNGP_RESPEC_PRIO", 0) ? lo : 0));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_g, hipEventDisableTiming));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_r, hipEventDisableTiming));
+        NNGP_HIP_CHECK(hipStreamCreateWithFlags(&r.st3, hipStreamNonBlocking));
+        NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_pre, hipEventDisableTiming));
+        NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_sel, hipEventDisableTiming));
+        NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_b, hipEventDisableTiming));
+        NNGP_HIP_CHECK(hipHostMalloc((void **)&r.herr, 64, hipHostMallocMapped | hipHostMallocCoherent));
         r.dev = dev;
     }
     while ((int)r.ev_q.size() < w) {
@@ -176,14 +188,21 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
     // stream while slice i's own fits run.  Their lists/fits form a second candidate set (hit = 2).
     const int W = spec ? (int)std::min<int64_t>(respec_window(), nq - 1) : 0;
     Respec *rs = nullptr;
-    if (W > 0) {
+    if (spec) {
         const int rc0 = respec_resources((size_t)nq, W, &rs);
         if (rc0) return rc0;
     }
+    // overlapped batch (NNGP_SPEC_OVERLAP, default 1; launch chain only): the batch's fits run on a
+    // side stream while the sweep starts as soon as the batch's neighbour lists exist; a hit slice's
+    // mean waits for that slice's fits only (per-prediction completion counters)
+    const bool chained = spec && chain_supported(sys, g_step_mode, m);
+    const bool overlap = spec && !chained && env_int("NNGP_SPEC_OVERLAP", 1) != 0 &&
+                         env_int("NNGP_RESPEC_PACKED", 0) == 0;
+    int32_t *done = nullptr;
     if (spec) {
         int err = 0;
         const size_t bytes = sizeof(double) * ((size_t)nq * d + d + (size_t)nq * n_fits * 4) +
-                             sizeof(int32_t) * ((size_t)nq * m + nq) +
+                             sizeof(int32_t) * ((size_t)nq * m + nq + nq) +
                              (W > 0 ? sizeof(double) * ((size_t)W * d + d + (size_t)nq * n_fits * 4) +
                                           sizeof(int32_t) * (size_t)nq * m
                                     : 0);
@@ -200,8 +219,9 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
         }
         spec_idx = (int32_t *)tail;
         flags = spec_idx + (size_t)nq * m;
+        done = flags + nq;   // [nq] (then spec2_idx)
         if (W > 0) {
-            spec2_idx = flags + nq;
+            spec2_idx = done + nq;
             NNGP_HIP_CHECK(hipMemsetAsync(spec2_idx, 0xFF, sizeof(int32_t) * (size_t)nq * m, st));   // -1: none
             for (int64_t j = 0; j < nq; j++) rs->hflags[j] = -1;
         }
@@ -213,9 +233,20 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
                 rc = nngp_parareal_update(d, UF + (size_t)(i + 1) * d, UG + (size_t)(i + 1) * d, gtmp,
                                           Qg + (j + 1) * d, stream);
         }
-        if (rc == NNGP_OK)
+        if (rc == NNGP_OK && overlap) {
+            *rs->herr = 0;
+            NNGP_HIP_CHECK(hipEventRecord(rs->ev_pre, st));             // the guesses Qg
+            NNGP_HIP_CHECK(hipStreamWaitEvent(rs->st3, rs->ev_pre, 0));
+            rc = spec_batch(X, Y, rows, d, Qg, (int)nq, m, n_jitter, jitter_exp_host, n_restarts, theta0, fatol,
+                            xatol, maxfev, spec_idx, spec_fits, false, rs->st3, 1, done, rs->ev_sel);
+            if (rc == NNGP_OK) {
+                NNGP_HIP_CHECK(hipEventRecord(rs->ev_b, rs->st3));
+                NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_sel, 0));   // lists ready; fits may run on
+            }
+        } else if (rc == NNGP_OK) {
             rc = spec_batch(X, Y, rows, d, Qg, (int)nq, m, n_jitter, jitter_exp_host, n_restarts, theta0, fatol,
                             xatol, maxfev, spec_idx, spec_fits, false, st);
+        }
         if (rc) return rc;
     }
     bool respec_pending = false;
@@ -226,7 +257,6 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
     std::vector<int> pend(split ? (size_t)nq : 0, -1);   // per slice: its window event, or -1
     // ---- the fused chain (nngp_gp.hip chain_kernel): runs of hit slices as one persistent kernel;
     // the host takes over at each miss (that slice's fits, the re-speculation), then resumes it
-    const bool chained = spec && chain_supported(sys, g_step_mode, m);
     if (chained) {
         float g_ms = 0.f;
         int i = I;
@@ -259,7 +289,7 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
                 if (rc == NNGP_OK)
                     rc = spec_batch(X, Y, rows, d, Qr, w, m, n_jitter, jitter_exp_host, n_restarts,
                                     theta0 + (j + 1) * n_fits * 2, fatol, xatol, maxfev, spec2_idx + (j + 1) * m,
-                                    spec2_fits + (j + 1) * n_fits * 4, env_int("NNGP_RESPEC_PACKED", 0) == 0, s2);
+                                    spec2_fits + (j + 1) * n_fits * 4, env_int("NNGP_RESPEC_PACKED", 0) == 0, s2, 6);
                 if (rc == NNGP_OK) {
                     NNGP_HIP_CHECK(hipEventRecord(rs->ev_r, s2));
                     respec_pending = true;
@@ -302,7 +332,8 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
                           xatol, maxfev, preds_scratch, ug_next, u_next, nullptr, spec ? spec_idx + j * m : nullptr,
                           spec ? spec_fits + j * n_fits * 4 : nullptr, spec ? flags + j : nullptr,
                           W > 0 ? spec2_idx + j * m : nullptr, W > 0 ? spec2_fits + j * n_fits * 4 : nullptr,
-                          (W > 0 && i + 1 < N) ? rs->hflags + j : nullptr, st);   // every written flag is awaited
+                          (W > 0 && i + 1 < N) ? rs->hflags + j : nullptr, st, 0, -1,   // every written flag is awaited
+                          overlap ? done + j : nullptr, overlap ? rs->herr : nullptr);
         if (rc || W == 0 || i + 1 >= N) continue;
         int32_t hit = 0;
         rc = wait_flag(rs->hflags + j, st, &hit);
@@ -328,7 +359,7 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
             for (int q = 0; q < w && rc == NNGP_OK; q++) {
                 rc = spec_batch(X, Y, rows, d, Qr + (size_t)q * d, 1, m, n_jitter, jitter_exp_host, n_restarts,
                                 theta0 + (j + 1 + q) * n_fits * 2, fatol, xatol, maxfev, spec2_idx + (j + 1 + q) * m,
-                                spec2_fits + (j + 1 + q) * n_fits * 4, env_int("NNGP_RESPEC_PACKED", 0) == 0, s2);
+                                spec2_fits + (j + 1 + q) * n_fits * 4, env_int("NNGP_RESPEC_PACKED", 0) == 0, s2, 6);
                 if (rc == NNGP_OK) {
                     NNGP_HIP_CHECK(hipEventRecord(rs->ev_q[q], s2));
                     pend[j + 1 + q] = q;
@@ -337,15 +368,23 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
         } else if (rc == NNGP_OK) {
             rc = spec_batch(X, Y, rows, d, Qr, w, m, n_jitter, jitter_exp_host, n_restarts,
                             theta0 + (j + 1) * n_fits * 2, fatol, xatol, maxfev, spec2_idx + (j + 1) * m,
-                            spec2_fits + (j + 1) * n_fits * 4, env_int("NNGP_RESPEC_PACKED", 0) == 0, s2);
+                            spec2_fits + (j + 1) * n_fits * 4, env_int("NNGP_RESPEC_PACKED", 0) == 0, s2, 6);
         }
         if (rc == NNGP_OK) {
             NNGP_HIP_CHECK(hipEventRecord(rs->ev_r, s2));
             respec_pending = true;
         }
     }
-    // the side stream never outlives the sweep (also on an error path: its buffers are reused)
+    // the side streams never outlive the sweep (also on an error path: their buffers are reused)
     if (respec_pending) NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_r, 0));
+    if (overlap) {
+        NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_b, 0));
+        NNGP_HIP_CHECK(hipStreamSynchronize(st));
+        if (rc == NNGP_OK && __atomic_load_n(rs->herr, __ATOMIC_ACQUIRE) != 0) {
+            set_error("correction sweep: a speculative fit count was not reached");
+            rc = NNGP_E_HIP;
+        }
+    }
     if (spec_hits_out && rc == NNGP_OK) {   // speculation hits (0 when not speculating)
         *spec_hits_out = 0;
         if (spec) {
