@@ -192,6 +192,8 @@ int nngp_predict_range(const double *X, const double *Y, int64_t rows, int d, co
  *     slice whose actual ordered kNN list equals its guess reuses those fits (bitwise identical:
  *     a fit depends only on the ordered neighbours, coordinate, jitter and theta0), the others
  *     are recomputed in the sweep.  Auto speculates while (N-I)*d*n_jitter*n_restarts <= 262144.
+ *     The batch's fits overlap the sweep on a side stream (a hit waits for its own prediction's
+ *     fits; NNGP_SPEC_OVERLAP=0 serialises them); the call returns after both have drained.
  *   spec_hits_out: HOST, number of slices served by the speculative batch, or NULL;
  *   g_ms_out: HOST, total device time of the G launches (ms), or NULL (no timing events).
  * With NNGP_CHAIN=1, speculation on, an ODE or Burgers (d = 64k <= 256) system, exact G and m <= 32, the runs
