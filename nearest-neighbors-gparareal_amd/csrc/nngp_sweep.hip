@@ -74,7 +74,9 @@ static int respec_resources(size_t nflags, int w, Respec **out) {
                                                    env_int("NNGP_RESPEC_PRIO", 0) ? lo : 0));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_g, hipEventDisableTiming));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_r, hipEventDisableTiming));
-        NNGP_HIP_CHECK(hipStreamCreateWithFlags(&r.st3, hipStreamNonBlocking));
+        // NNGP_BATCH_PRIO: 1 = the overlapped batch at the least priority (the sweep's kernels first)
+        NNGP_HIP_CHECK(hipStreamCreateWithPriority(&r.st3, hipStreamNonBlocking,
+                                                   env_int("NNGP_BATCH_PRIO", 0) ? lo : 0));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_pre, hipEventDisableTiming));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_sel, hipEventDisableTiming));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_b, hipEventDisableTiming));
