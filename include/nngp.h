@@ -221,6 +221,12 @@ int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mode
  * misses finished by the host's fits.  Returns launches; *slices_out (HOST, optional). */
 int64_t nngp_chain_stats(int64_t *slices_out);
 
+/* Drains the device and releases every resource the library holds (workspaces, side streams,
+ * events, host-mapped flags); the next call re-creates what it needs.  Registered with atexit
+ * by the Python package, so none of them is left to the HIP runtime's process-exit teardown.
+ * (No reference counterpart: the reference holds no device resources.)  Returns 0. */
+int nngp_shutdown(void);
+
 /* ---- 4. full-data GParareal (models.GPjax_p, models.py:273-473) ------------------------------
  * The training set X, Y: DEVICE [rows][d], rows <= 7936.  K = sigma_y^2 exp(-0.5/sigma_x^2 D^2)
  * + 10^jitter I over ALL rows (kernel_np / _fit_gp_np, models.py:300-312), theta = (sigma_x,

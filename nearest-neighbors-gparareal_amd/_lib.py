@@ -23,7 +23,7 @@ STEP_FIXED, STEP_LINSPACE, STEP_CONTRACT = 0, 1, 16
 EXPORTS = ['nngp_abi_version', 'nngp_last_error', 'nngp_device_count', 'nngp_rk_batch', 'nngp_rk_batch_grid',
            'nngp_rhs_batch', 'nngp_parareal_update', 'nngp_knn', 'nngp_nm_fit_batch',
            'nngp_gp_mean', 'nngp_predict', 'nngp_correction_sweep', 'nngp_gpfull_lml', 'nngp_gpfull_fit',
-           'nngp_gpfull_mean', 'nngp_predict_range', 'nngp_chain_stats']
+           'nngp_gpfull_mean', 'nngp_predict_range', 'nngp_chain_stats', 'nngp_shutdown']
 MODEL_PARAREAL, MODEL_NNGP, MODEL_GPFULL = 0, 1, 2
 
 
@@ -103,12 +103,21 @@ def host_doubles(a):
     return a, a.ctypes.data_as(_dp)
 
 
+_shutdown_registered = False
+
+
 def require_gpu():
-    """The product path runs on the GPU only; fail loudly otherwise."""
+    """The product path runs on the GPU only; fail loudly otherwise.  The first call registers
+    nngp_shutdown with atexit (it runs before torch's and the HIP runtime's own teardown)."""
+    global _shutdown_registered
     import torch
     if not torch.cuda.is_available():
         raise NNGPError('no HIP device visible: nnGParareal-amd has no CPU fallback')
-    lib()
+    L = lib()
+    if not _shutdown_registered:
+        import atexit
+        atexit.register(L.nngp_shutdown)
+        _shutdown_registered = True
     return torch
 
 

@@ -5,11 +5,18 @@
 #include <stdint.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/nngp.h"
 
 namespace nngp {
+
+// integer tuning/test knob from the environment (read on every call: tests toggle them in-process)
+inline int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
 
 // thread-local last error, returned by nngp_last_error()
 void set_error(const char *fmt, ...);
@@ -48,8 +55,9 @@ void set_error(const char *fmt, ...);
 // speculative sweep's batch buffers, which must outlive the per-slice calls.  Growing a slot
 // frees the old buffer after hipFree's implicit device synchronisation.  Not thread-safe across
 // host threads sharing a device.
-constexpr int N_WS_SLOTS = 7;   // slot 2: the sweep's speculation buffers; 3: full-GP factors; 4: fit queues; 5: parked fits;
-                                // 6: the re-speculation window's batch (slot 1 may still be read by an overlapped batch)
+constexpr int N_WS_SLOTS = 9;   // slot 2: the sweep's speculation buffers; 3: full-GP factors; 4: fit queues; 5: parked fits;
+                                // 6: the re-speculation window's batch (slot 1 may still be read by an overlapped batch);
+                                // 7 / 8: the fit queues of the overlapped batch / of the re-speculation window
 void *workspace(size_t bytes, int *err, int slot = 0);
 
 int predict_impl(const double *X, const double *Y, int64_t rows, int d, const double *new_x, int m,
@@ -66,6 +74,8 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
                double fatol, double xatol, int maxfev, int32_t *idx_out, double *fits_out, bool latency,
                hipStream_t st, int slot = 1, int32_t *done = nullptr, hipEvent_t ev_select = nullptr);
 // the fused correction chain (nngp_gp.hip): one persistent kernel per run of hit slices
+void chain_release();   // nngp_shutdown's parts (nngp_gp.hip / nngp_sweep.hip)
+void sweep_release();
 bool chain_supported(const nngp_system *sys, int g_step_mode, int m);
 int chain_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps, const double *t, int I,
                 int N, int i0, double *U1, double *UG1, const double *X, const double *Y, int64_t rows, int m,

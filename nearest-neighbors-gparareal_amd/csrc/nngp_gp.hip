@@ -273,8 +273,7 @@ static inline size_t knn_xs_bytes(int m, int64_t d) { return (size_t)knn_xs_doub
 // D2/kd2 by d2_wave_kernel (a wave per pair) where the select's own pass would leave one lane per
 // pair walking d terms from global memory: d > 128 or rows not staged.  NNGP_D2_WAVES=0: never.
 static inline bool d2_by_waves(int m, int d) {
-    static const int env = getenv("NNGP_D2_WAVES") ? atoi(getenv("NNGP_D2_WAVES")) : 1;
-    return env != 0 && (d > 128 || knn_xs_doubles(m, d) == 0);
+    return env_int("NNGP_D2_WAVES", 1) != 0 && (d > 128 || knn_xs_doubles(m, d) == 0);
 }
 
 // LDS of one select (the caller's: a kernel-level __shared__ object, one per kernel)
@@ -1176,17 +1175,9 @@ __device__ __forceinline__ double jit_lookup(const NMArgs &a, int j) {
 template <int MAXM> struct NMBound { static constexpr int T = (MAXM <= 16) ? 512 : (MAXM <= 32 ? 256 : 64); };
 // threads of the wave-per-fit speculative kernel and of the mean kernel
 template <int MAXM> struct WGT { static constexpr int T = MAXM > 32 ? 64 : 256; };
-// minimum waves per SIMD the fits kernels are register-allocated for (NNGP_NM_WAVES at build time;
-// 1 = no constraint).  MAXM <= 16 takes ~180 VGPRs (2 waves); -DNNGP_NM_WAVES=3 caps them at 168
-// with 84-108 bytes of spills: measured slower (Burgers N=128 0.305 -> 0.314-0.321 s, d=128
-// correction 0.626 -> 0.702 ms), so not kept
-#ifndef NNGP_NM_WAVES
-#define NNGP_NM_WAVES 1
-#endif
-template <int MAXM> struct NMWaves { static constexpr int W = MAXM <= 16 ? NNGP_NM_WAVES : 1; };
 
 template <int MAXM, bool FUSED>
-__global__ void __launch_bounds__(NMBound<MAXM>::T, NMWaves<MAXM>::W) nm_fit_kernel(NMArgs a) {
+__global__ void __launch_bounds__(NMBound<MAXM>::T) nm_fit_kernel(NMArgs a) {
     constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG;
     extern __shared__ __attribute__((aligned(16))) double sm[];
     if (a.skip && *a.skip) return;   // uniform: the whole grid exits
@@ -1386,7 +1377,7 @@ __device__ __forceinline__ int nm_candidates(const NM &S, NMCand (&c)[4]) {
 }
 
 template <int MAXM>
-__global__ void __launch_bounds__(WGT<MAXM>::T, NMWaves<MAXM>::W) nm_spec_kernel(NMArgs a) {
+__global__ void __launch_bounds__(WGT<MAXM>::T) nm_spec_kernel(NMArgs a) {
     constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG;
     extern __shared__ __attribute__((aligned(16))) double sm[];
     if (a.skip && *a.skip) return;   // uniform: the whole grid exits (speculation hit)
@@ -1502,18 +1493,24 @@ __device__ __forceinline__ void gp_mean_dev(const NMArgs &a, int blk, bool load_
     double *sD2 = sm, *skd2 = sm + m * m, *sK = skd2 + m;
     const int tid = threadIdx.x, g = tid / 16, l = tid % 16;
     if (a.wait_done) {   // a hit served by the overlapped batch: wait for its fits of this query
-        if (tid == 0 && __hip_atomic_load(a.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
-            uint32_t spin = 0;
-            while (__hip_atomic_load(a.wait_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.wait_n) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++spin > (1u << 24)) {   // never a hang: report and go on
-                    __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    break;
+        __shared__ int s_late;
+        if (tid == 0) {
+            s_late = 0;
+            if (__hip_atomic_load(a.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+                uint32_t spin = 0;
+                while (__hip_atomic_load(a.wait_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.wait_n) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spin > (1u << 24)) {   // never a hang: flag it, write nothing; the host
+                        s_late = 1;              // redoes the sweep without the overlap
+                        __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        break;
+                    }
                 }
+                __threadfence();
             }
-            __threadfence();
         }
         __syncthreads();
+        if (s_late) return;
     }
     if (load_lds) {
         for (int i = tid; i < m * m; i += blockDim.x) sD2[i] = a.D2[i];
@@ -1571,7 +1568,7 @@ __global__ void __launch_bounds__(WGT<MAXM>::T) gp_mean_kernel(NMArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // Fused correction chain (reference parareal.py:359-382): the speculative
-// sweep's per-slice hit path as ONE persistent cooperative kernel.  For i = i0, i0+1, ...:
+// sweep's per-slice hit path as ONE persistent kernel.  For i = i0, i0+1, ...:
 //   1. G:      UG1[i+1] = G(U1[i])            workgroup 0 (one lane for an ODE, one wave for Burgers)
 //   2. kNN:    distances of every training row to U1[i]                    all workgroups
 //   3. select: the ordered m-neighbour list, y_m, D2, kd2; hit = list == the speculative batch's
@@ -1617,7 +1614,7 @@ struct ChainArgs {
     uint64_t *prof;            // host-mapped [4] or null (NNGP_CHAIN_PROF): ticks in G | kNN | select | mean
 };
 
-// all workgroups of the (cooperative, co-resident) grid: arrivals counted on one agent-scope
+// all workgroups of the (co-resident) grid: arrivals counted on one agent-scope
 // counter; the fences make every workgroup's global writes before the barrier visible to every
 // workgroup after it (L2 write-back / invalidate across the XCDs)
 __device__ __forceinline__ void chain_barrier(uint32_t *bar, uint32_t &target) {
@@ -1907,11 +1904,7 @@ static int run_nm_spec(NMArgs &a, hipStream_t st, int nq = 1) {
 // 2304; m=20 spec wins at 864 fits (0.67 vs 0.98 ms), loses from 1152 (1.10 vs 0.98 ms).
 // NNGP_NM_SPEC=0/1 forces either (tuning).
 static bool use_spec(int n_fits, int m) {
-    static int forced = -2;
-    if (forced == -2) {
-        const char *e = getenv("NNGP_NM_SPEC");
-        forced = e ? atoi(e) : -1;
-    }
+    const int forced = env_int("NNGP_NM_SPEC", -1);
     if (forced >= 0) return forced != 0;
     static int ncu = 0;
     if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) ncu = 256;
@@ -1922,16 +1915,12 @@ static bool use_spec(int n_fits, int m) {
 
 // fits per 16-lane group in the unfused kernel's work-queue mode (NNGP_NM_REFILL; 0/1 = off)
 static int nm_fits_per_row() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("NNGP_NM_REFILL");
-        v = e ? atoi(e) : 8;
-        if (v < 0) v = 0;
-    }
-    return v;
+    return std::max(0, env_int("NNGP_NM_REFILL", 8));
 }
 
-static int run_nm(NMArgs &a, bool fused, hipStream_t st, int nq = 1) {
+// qslot: the workspace slot of the work-queue counters -- its own per concurrent stream (the
+// sweep's fits: 4; the overlapped speculative batch: 7; the re-speculation window: 8)
+static int run_nm(NMArgs &a, bool fused, hipStream_t st, int nq = 1, int qslot = 4) {
     const int maxm = maxm_for(a.m);
     const size_t kimg = k_image_doubles(maxm);
     const int tmax = maxm <= 16 ? NMBound<16>::T : (maxm <= 32 ? NMBound<32>::T : NMBound<64>::T);
@@ -1972,7 +1961,7 @@ static int run_nm(NMArgs &a, bool fused, hipStream_t st, int nq = 1) {
         const int per_row = nm_fits_per_row();
         if (per_row > 1 && nblocks > 1) {   // work queues: ~per_row fits per group on average
             int err = 0;
-            int32_t *qbuf = (int32_t *)workspace(sizeof(int32_t) * (size_t)nq, &err, 4);
+            int32_t *qbuf = (int32_t *)workspace(sizeof(int32_t) * (size_t)nq, &err, qslot);
             if (err) return err;
             NNGP_HIP_CHECK(hipMemsetAsync(qbuf, 0, sizeof(int32_t) * (size_t)nq, st));
             a.queue = qbuf;
@@ -1988,9 +1977,7 @@ static int run_nm(NMArgs &a, bool fused, hipStream_t st, int nq = 1) {
 // evaluation count at which the packed kernel parks a fit for the speculative kernel
 // (NNGP_NM_PARK; 0 = never)
 static int nm_park_cap() {
-    const char *e = getenv("NNGP_NM_PARK");
-    const int v = e ? atoi(e) : 70;
-    return v < 0 ? 0 : v;
+    return std::max(0, env_int("NNGP_NM_PARK", 70));
 }
 
 // packed fits of ONE prediction with the tail hand-off: fits still running at nm_park_cap()
@@ -2008,7 +1995,7 @@ static int run_nm_parked(NMArgs a, hipStream_t st) {
     // jitter-major rows (NNGP_NM_JMAJOR=0: product order): fits sharing a jitter run similar
     // evaluation counts, so a wave's rows finish together (d = 800 synthetic correction
     // 2.99 -> 2.72 ms; profiles/r02/jmajor_probe.txt)
-    a.jmajor = getenv("NNGP_NM_JMAJOR") ? atoi(getenv("NNGP_NM_JMAJOR")) : 1;
+    a.jmajor = env_int("NNGP_NM_JMAJOR", 1);
     a.park = park;
     a.park_count = cnt;
     a.park_list = cnt + 1;
@@ -2207,6 +2194,7 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
     if (err) return err;
     double *D2 = dist + (size_t)nq * rows;
     double *ymT = D2 + (size_t)nq * m * m;
+    if (done) NNGP_HIP_CHECK(hipMemsetAsync(done, 0, sizeof(int32_t) * (size_t)nq, st));
     hipLaunchKernelGGL(knn_dist_kernel, dim3((unsigned)((rows + 63) / 64), (unsigned)nq), dim3(64), 0, st, X,
                        rows, d, Q, dist);
     NNGP_LAUNCH_CHECK();
@@ -2221,24 +2209,23 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
                            idx_out, m, d, Q, D2, (double *)nullptr);
         NNGP_LAUNCH_CHECK();
     }
+    // the counters are zeroed (above) before the event the sweep's mean kernels wait behind
     if (ev_select) NNGP_HIP_CHECK(hipEventRecord(ev_select, st));   // the lists are ready
-    if (done) NNGP_HIP_CHECK(hipMemsetAsync(done, 0, sizeof(int32_t) * (size_t)nq, st));
     a.m = m; a.d = d; a.n_fits = (int)nfp;
     a.D2 = D2; a.Y = ymT; a.ys_c = m; a.ys_r = 1;
     a.theta0 = theta0; a.fatol = fatol; a.xatol = xatol; a.maxfev = maxfev; a.R = n_restarts;
     a.fits_out = fits_out;
     a.qs_D2 = (int64_t)m * m; a.qs_Y = (int64_t)d * m; a.qs_th = (int64_t)nfp * 2; a.qs_fits = (int64_t)nfp * 4;
-    a.jmajor = getenv("NNGP_NM_JMAJOR") ? atoi(getenv("NNGP_NM_JMAJOR")) : 1;   // (run_nm_parked; Burgers 0.328 -> 0.317 s)
+    a.jmajor = env_int("NNGP_NM_JMAJOR", 1);   // (run_nm_parked; Burgers 0.328 -> 0.317 s)
     a.done = done;
     // latency: a wave per fit (the re-speculation window the sweep waits on); else packed fits
     if (latency) return run_nm_spec(a, st, nq);
-    return run_nm(a, false, st, nq);
+    return run_nm(a, false, st, nq, slot == 1 ? 7 : 8);
 }
 
 // ---- the fused correction chain, host side ----------------------------------------------------
 struct ChainRes {
     int dev = -1;
-    int coop = 0;             // cooperative launches supported
     double tick_khz = 0;      // wall_clock64 rate
     uint32_t *bar = nullptr;  // device: grid-barrier counter
     int32_t *stop = nullptr;  // host-mapped: stop slice | G ticks (u64)
@@ -2246,6 +2233,14 @@ struct ChainRes {
 static ChainRes g_chain;
 static std::mutex g_chain_mu;
 static int64_t g_chain_launches = 0, g_chain_slices = 0;   // nngp_chain_stats (under g_chain_mu)
+
+// nngp_shutdown: release the chain's buffers (re-created on next use)
+void chain_release() {
+    std::lock_guard<std::mutex> lk(g_chain_mu);
+    if (g_chain.bar) (void)hipFree(g_chain.bar);
+    if (g_chain.stop) (void)hipHostFree(g_chain.stop);
+    g_chain = ChainRes{};
+}
 
 static int chain_resources(ChainRes **out) {
     std::lock_guard<std::mutex> lk(g_chain_mu);
@@ -2256,7 +2251,6 @@ static int chain_resources(ChainRes **out) {
         if (r.bar) (void)hipFree(r.bar);
         if (r.stop) (void)hipHostFree(r.stop);
         r = ChainRes{};
-        NNGP_HIP_CHECK(hipDeviceGetAttribute(&r.coop, hipDeviceAttributeCooperativeLaunch, dev));
         int khz = 0;
         NNGP_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
         r.tick_khz = khz > 0 ? khz : 100000.0;
@@ -2288,11 +2282,22 @@ bool chain_supported(const nngp_system *sys, int g_step_mode, int m) {
     }
 }
 
+// An ordinary launch.  The grid barrier needs every workgroup resident at once: nb <= 64
+// workgroups of 256 threads, checked against the kernel's occupancy, and nothing else runs on the
+// device meanwhile (the overlapped batch is off in chain mode; the re-speculation window is
+// launched only after the kernel has drained) -- and a workgroup that had to wait for a CU would
+// still be scheduled once the kernels ahead of it finish, since none of them waits on the chain.
+// (A cooperative launch gave the same guarantee through a separate HIP device queue, whose
+// teardown at process exit crashed under rocprofv3: profiles/r03/chain_exit_crash.txt.)
 template <int MAXM>
 static int chain_launch(ChainArgs &c, int nb, size_t lds, hipStream_t st) {
-    void *args[] = {&c};
-    NNGP_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&chain_kernel<MAXM>), dim3(nb),
-                                              dim3(256), args, (unsigned)lds, st));
+    static int ncu = 0;
+    if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) ncu = 0;
+    int per_cu = 0;
+    NNGP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<MAXM>, 256, lds));
+    NNGP_REQUIRE(per_cu >= 1 && (int64_t)per_cu * ncu >= nb, "chain: %d workgroups cannot be co-resident", nb);
+    hipLaunchKernelGGL(chain_kernel<MAXM>, dim3(nb), dim3(256), lds, st, c);
+    NNGP_LAUNCH_CHECK();
     return NNGP_OK;
 }
 
@@ -2309,7 +2314,6 @@ int chain_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t 
     ChainRes *res = nullptr;
     int rc = chain_resources(&res);
     if (rc) return rc;
-    NNGP_REQUIRE(res->coop, "chain: cooperative launches unsupported on this device");
     ChainArgs c{};
     rc = fill_jitters(c.a, n_jitter, jitter_exp_host);
     if (rc) return rc;
@@ -2359,16 +2363,15 @@ int chain_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t 
     c.bar = res->bar;
     c.stop = res->stop;
     c.g_ticks = (uint64_t *)(res->stop + 2);
-    static const bool prof = getenv("NNGP_CHAIN_PROF") && atoi(getenv("NNGP_CHAIN_PROF"));
+    const bool prof = env_int("NNGP_CHAIN_PROF", 0) != 0;
     c.prof = prof ? (uint64_t *)(res->stop + 4) : nullptr;
     const int maxm = maxm_for(m);
     const size_t lds = std::max(knn_xs_bytes(m, d),
                                 sizeof(double) * ((size_t)m * m + m + 16 * k_image_doubles(maxm)));
     NNGP_REQUIRE(lds + sizeof(SelShm) + sizeof(double) * CHAIN_QMAX <= 160 * 1024, "chain: LDS");
-    // workgroups: one per 16 coordinates of the mean phase (NNGP_CHAIN_WGS overrides; 1 = no grid
-    // barrier at all)
-    static const int wgs_env = getenv("NNGP_CHAIN_WGS") ? atoi(getenv("NNGP_CHAIN_WGS")) : 0;
-    const int nb = std::max(1, std::min(wgs_env > 0 ? wgs_env : c.n_mean_blk, 64));
+    // workgroups: one per 16 coordinates of the mean phase (a single workgroup, i.e. no grid
+    // barrier, measured slower: 65 us per slice, 0.387 s for Burgers N=128)
+    const int nb = std::max(1, std::min(c.n_mean_blk, 64));
     res->stop[0] = -1;
     NNGP_HIP_CHECK(hipMemsetAsync(res->bar, 0, sizeof(uint32_t), st));
     switch (maxm) {

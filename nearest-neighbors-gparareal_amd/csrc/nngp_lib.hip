@@ -53,7 +53,29 @@ void *workspace(size_t bytes, int *err, int slot) {
     return w.ptr;
 }
 
+// nngp_shutdown: free every workspace slot (re-allocated on next use)
+static void ws_release() {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    for (Ws &w : g_ws)
+        if (w.ptr) (void)hipFree(w.ptr);
+    g_ws.clear();
+}
+
 }  // namespace nngp
+
+// Release every device / host-mapped resource the library holds (workspaces, side streams,
+// events, the fused chain's flags) after draining the device, so that nothing of ours is left
+// for the HIP runtime's own process-exit teardown.  The Python package registers it with atexit;
+// later calls simply re-create what they need.
+extern "C" int nngp_shutdown(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return NNGP_OK;
+    (void)hipDeviceSynchronize();
+    nngp::chain_release();
+    nngp::sweep_release();
+    nngp::ws_release();
+    return NNGP_OK;
+}
 
 extern "C" int nngp_abi_version(void) { return NNGP_ABI_VERSION; }
 

@@ -30,9 +30,11 @@ static int timing_events(size_t n, hipEvent_t **out) {
     return NNGP_OK;
 }
 
-static int env_int(const char *name, int dflt) {
-    const char *e = getenv(name);
-    return e ? atoi(e) : dflt;
+// nngp_shutdown: the sweep's timing events (re-created on next use)
+static void events_release() {
+    std::lock_guard<std::mutex> lk(g_events_mu);
+    for (hipEvent_t e : g_events) (void)hipEventDestroy(e);
+    g_events.clear();
 }
 
 // re-speculation resources (per process; one device per process): a side stream, the events
@@ -41,7 +43,6 @@ struct Respec {
     int dev = -1;
     hipStream_t st2 = nullptr;
     hipEvent_t ev_g = nullptr, ev_r = nullptr;
-    std::vector<hipEvent_t> ev_q;   // per query of the window (split re-speculation)
     hipStream_t st3 = nullptr;      // the overlapped speculative batch
     hipEvent_t ev_pre = nullptr, ev_sel = nullptr, ev_b = nullptr;
     int32_t *herr = nullptr;        // host-mapped: a mean kernel's wait timed out
@@ -51,7 +52,7 @@ struct Respec {
 static Respec g_respec;
 static std::mutex g_respec_mu;
 
-static int respec_resources(size_t nflags, int w, Respec **out) {
+static int respec_resources(size_t nflags, Respec **out) {
     std::lock_guard<std::mutex> lk(g_respec_mu);
     Respec &r = g_respec;
     int dev = 0;
@@ -60,33 +61,21 @@ static int respec_resources(size_t nflags, int w, Respec **out) {
         if (r.st2) (void)hipStreamDestroy(r.st2);
         if (r.ev_g) (void)hipEventDestroy(r.ev_g);
         if (r.ev_r) (void)hipEventDestroy(r.ev_r);
-        for (hipEvent_t e : r.ev_q) (void)hipEventDestroy(e);
         if (r.st3) (void)hipStreamDestroy(r.st3);
         for (hipEvent_t e : {r.ev_pre, r.ev_sel, r.ev_b})
             if (e) (void)hipEventDestroy(e);
         if (r.herr) (void)hipHostFree(r.herr);
         if (r.hflags) (void)hipHostFree(r.hflags);
         r = Respec{};
-        int lo = 0, hi = 0;
-        NNGP_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        // NNGP_RESPEC_PRIO: 0 = default priority, 1 = the least priority (the sweep's own fits first)
-        NNGP_HIP_CHECK(hipStreamCreateWithPriority(&r.st2, hipStreamNonBlocking,
-                                                   env_int("NNGP_RESPEC_PRIO", 0) ? lo : 0));
+        NNGP_HIP_CHECK(hipStreamCreateWithFlags(&r.st2, hipStreamNonBlocking));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_g, hipEventDisableTiming));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_r, hipEventDisableTiming));
-        // NNGP_BATCH_PRIO: 1 = the overlapped batch at the least priority (the sweep's kernels first)
-        NNGP_HIP_CHECK(hipStreamCreateWithPriority(&r.st3, hipStreamNonBlocking,
-                                                   env_int("NNGP_BATCH_PRIO", 0) ? lo : 0));
+        NNGP_HIP_CHECK(hipStreamCreateWithFlags(&r.st3, hipStreamNonBlocking));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_pre, hipEventDisableTiming));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_sel, hipEventDisableTiming));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_b, hipEventDisableTiming));
         NNGP_HIP_CHECK(hipHostMalloc((void **)&r.herr, 64, hipHostMallocMapped | hipHostMallocCoherent));
         r.dev = dev;
-    }
-    while ((int)r.ev_q.size() < w) {
-        hipEvent_t e;
-        NNGP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        r.ev_q.push_back(e);
     }
     if (r.nflags < nflags) {
         if (r.hflags) (void)hipHostFree(r.hflags);
@@ -98,6 +87,20 @@ static int respec_resources(size_t nflags, int w, Respec **out) {
     }
     *out = &r;
     return NNGP_OK;
+}
+
+// nngp_shutdown: the side streams, events and host-mapped flags (re-created on next use)
+void sweep_release() {
+    events_release();
+    std::lock_guard<std::mutex> lk(g_respec_mu);
+    Respec &r = g_respec;
+    if (r.st2) (void)hipStreamDestroy(r.st2);
+    if (r.st3) (void)hipStreamDestroy(r.st3);
+    for (hipEvent_t e : {r.ev_g, r.ev_r, r.ev_pre, r.ev_sel, r.ev_b})
+        if (e) (void)hipEventDestroy(e);
+    if (r.herr) (void)hipHostFree(r.herr);
+    if (r.hflags) (void)hipHostFree(r.hflags);
+    r = Respec{};
 }
 
 // wait for the select kernel's host-mapped hit flag (-1 = not yet written); a stream that has
@@ -125,9 +128,7 @@ static int wait_flag(const int32_t *flag, hipStream_t st, int32_t *out) {
 
 // slices re-speculated after a miss (NNGP_RESPEC_W; 0 disables)
 static int respec_window() {
-    const char *e = getenv("NNGP_RESPEC_W");
-    const int w = e ? atoi(e) : 4;
-    return w < 0 ? 0 : w;
+    return std::max(0, env_int("NNGP_RESPEC_W", 4));
 }
 
 }  // namespace nngp
@@ -138,23 +139,19 @@ static int respec_window() {
 static bool speculate_ok(int speculate, int64_t nq, int64_t n_fits) {
     if (speculate == 0 || nq < 2) return false;
     if (speculate > 0) return true;
-    static int64_t bound = -1;
-    if (bound < 0) {
-        const char *e = getenv("NNGP_SPEC_MAX_FITS");
-        bound = e ? atoll(e) : 262144;
-    }
+    const char *e = getenv("NNGP_SPEC_MAX_FITS");
+    const int64_t bound = e ? atoll(e) : 262144;
     return nq * n_fits <= bound;
 }
 
-extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mode,
-                                     int64_t g_steps, const double *t, int I, int N, double *U1,
-                                     double *UG1, const double *UF, const double *UG, int model,
-                                     const double *X, const double *Y, int64_t rows, int m,
-                                     int n_jitter, const double *jitter_exp_host, int n_restarts,
-                                     const double *theta0, double fatol, double xatol, int maxfev,
-                                     double *preds_scratch, int speculate, int32_t *spec_hits_out,
-                                     float *g_ms_out, void *stream) {
+static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps,
+                            const double *t, int I, int N, double *U1, double *UG1, const double *UF,
+                            const double *UG, int model, const double *X, const double *Y, int64_t rows, int m,
+                            int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
+                            double fatol, double xatol, int maxfev, double *preds_scratch, int speculate,
+                            int32_t *spec_hits_out, float *g_ms_out, void *stream, bool allow_overlap, int *late) {
     using namespace nngp;
+    *late = 0;
     NNGP_REQUIRE(sys != nullptr && t && U1 && UG1, "null argument");
     NNGP_REQUIRE(0 <= I && I <= N, "need 0 <= I <= N (I=%d N=%d)", I, N);
     NNGP_REQUIRE(model == NNGP_MODEL_PARAREAL || model == NNGP_MODEL_NNGP || model == NNGP_MODEL_GPFULL,
@@ -191,15 +188,14 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
     const int W = spec ? (int)std::min<int64_t>(respec_window(), nq - 1) : 0;
     Respec *rs = nullptr;
     if (spec) {
-        const int rc0 = respec_resources((size_t)nq, W, &rs);
+        const int rc0 = respec_resources((size_t)nq, &rs);
         if (rc0) return rc0;
     }
     // overlapped batch (NNGP_SPEC_OVERLAP, default 1; launch chain only): the batch's fits run on a
     // side stream while the sweep starts as soon as the batch's neighbour lists exist; a hit slice's
     // mean waits for that slice's fits only (per-prediction completion counters)
     const bool chained = spec && chain_supported(sys, g_step_mode, m);
-    const bool overlap = spec && !chained && env_int("NNGP_SPEC_OVERLAP", 1) != 0 &&
-                         env_int("NNGP_RESPEC_PACKED", 0) == 0;
+    const bool overlap = spec && !chained && allow_overlap && env_int("NNGP_SPEC_OVERLAP", 1) != 0;
     int32_t *done = nullptr;
     if (spec) {
         int err = 0;
@@ -252,11 +248,6 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
         if (rc) return rc;
     }
     bool respec_pending = false;
-    // NNGP_RESPEC_SPLIT (default 0): the window's re-speculation as one launch set per slice, each
-    // slice waiting for its own (launch chain only).  Measured slower (Burgers N=128 0.297 -> 0.413
-    // s): on one side stream the sets run one after another instead of as one parallel launch
-    const bool split = W > 0 && env_int("NNGP_RESPEC_SPLIT", 0) != 0;
-    std::vector<int> pend(split ? (size_t)nq : 0, -1);   // per slice: its window event, or -1
     // ---- the fused chain (nngp_gp.hip chain_kernel): runs of hit slices as one persistent kernel;
     // the host takes over at each miss (that slice's fits, the re-speculation), then resumes it
     if (chained) {
@@ -291,7 +282,7 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
                 if (rc == NNGP_OK)
                     rc = spec_batch(X, Y, rows, d, Qr, w, m, n_jitter, jitter_exp_host, n_restarts,
                                     theta0 + (j + 1) * n_fits * 2, fatol, xatol, maxfev, spec2_idx + (j + 1) * m,
-                                    spec2_fits + (j + 1) * n_fits * 4, env_int("NNGP_RESPEC_PACKED", 0) == 0, s2, 6);
+                                    spec2_fits + (j + 1) * n_fits * 4, true, s2, 6);
                 if (rc == NNGP_OK) {
                     NNGP_HIP_CHECK(hipEventRecord(rs->ev_r, s2));
                     respec_pending = true;
@@ -322,13 +313,8 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
         }
         if (W > 0) {
             NNGP_HIP_CHECK(hipEventRecord(rs->ev_g, st));                  // G(U1[i]) done
-            if (split) {   // this slice's re-speculated list/fits ready (not the whole window's)
-                if (pend[j] >= 0) NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_q[pend[j]], 0));
-                pend[j] = -1;
-            } else {
-                if (respec_pending) NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_r, 0));   // lists/fits ready
-                respec_pending = false;
-            }
+            if (respec_pending) NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_r, 0));   // lists/fits ready
+            respec_pending = false;
         }
         rc = predict_impl(X, Y, rows, d, ui, m, n_jitter, jitter_exp_host, n_restarts, theta0 + j * n_fits * 2, fatol,
                           xatol, maxfev, preds_scratch, ug_next, u_next, nullptr, spec ? spec_idx + j * m : nullptr,
@@ -354,24 +340,10 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
                 rc = nngp_parareal_update(d, UF + (size_t)(s + 1) * d, UG + (size_t)(s + 1) * d, g2,
                                           Qr + (size_t)q * d, s2);
         }
-        if (rc == NNGP_OK && split) {
-            // one launch set per guessed slice, nearest first, each with its own event: slice i+1
-            // waits for its own fits only, not for the window's (they otherwise finish together,
-            // throughput-bound, behind this miss's own fits)
-            for (int q = 0; q < w && rc == NNGP_OK; q++) {
-                rc = spec_batch(X, Y, rows, d, Qr + (size_t)q * d, 1, m, n_jitter, jitter_exp_host, n_restarts,
-                                theta0 + (j + 1 + q) * n_fits * 2, fatol, xatol, maxfev, spec2_idx + (j + 1 + q) * m,
-                                spec2_fits + (j + 1 + q) * n_fits * 4, env_int("NNGP_RESPEC_PACKED", 0) == 0, s2, 6);
-                if (rc == NNGP_OK) {
-                    NNGP_HIP_CHECK(hipEventRecord(rs->ev_q[q], s2));
-                    pend[j + 1 + q] = q;
-                }
-            }
-        } else if (rc == NNGP_OK) {
+        if (rc == NNGP_OK)   // a wave per fit: the sweep waits on this window's fits
             rc = spec_batch(X, Y, rows, d, Qr, w, m, n_jitter, jitter_exp_host, n_restarts,
                             theta0 + (j + 1) * n_fits * 2, fatol, xatol, maxfev, spec2_idx + (j + 1) * m,
-                            spec2_fits + (j + 1) * n_fits * 4, env_int("NNGP_RESPEC_PACKED", 0) == 0, s2, 6);
-        }
+                            spec2_fits + (j + 1) * n_fits * 4, true, s2, 6);
         if (rc == NNGP_OK) {
             NNGP_HIP_CHECK(hipEventRecord(rs->ev_r, s2));
             respec_pending = true;
@@ -383,7 +355,10 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
         NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_b, 0));
         NNGP_HIP_CHECK(hipStreamSynchronize(st));
         if (rc == NNGP_OK && __atomic_load_n(rs->herr, __ATOMIC_ACQUIRE) != 0) {
-            set_error("correction sweep: a speculative fit count was not reached");
+            // a hit slice's mean gave up waiting for the batch's fits (bounded spin; e.g. a GPU
+            // shared by several ranks) and wrote nothing: the caller redoes the sweep serially
+            set_error("correction sweep: a speculative fit count was not reached in time");
+            *late = 1;
             rc = NNGP_E_HIP;
         }
     }
@@ -406,5 +381,27 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
         }
         *g_ms_out = total;
     }
+    return rc;
+}
+
+extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mode,
+                                     int64_t g_steps, const double *t, int I, int N, double *U1,
+                                     double *UG1, const double *UF, const double *UG, int model,
+                                     const double *X, const double *Y, int64_t rows, int m,
+                                     int n_jitter, const double *jitter_exp_host, int n_restarts,
+                                     const double *theta0, double fatol, double xatol, int maxfev,
+                                     double *preds_scratch, int speculate, int32_t *spec_hits_out,
+                                     float *g_ms_out, void *stream) {
+    // The sweep writes UG1[i+1] and U1[i+1] for i >= I only and reads none of them before writing,
+    // so a sweep whose overlapped batch fell behind (see correction_sweep) is simply run again
+    // with the batch serialised: the same bits, later.
+    int late = 0;
+    int rc = correction_sweep(sys, g_tableau, g_step_mode, g_steps, t, I, N, U1, UG1, UF, UG, model, X, Y, rows, m,
+                              n_jitter, jitter_exp_host, n_restarts, theta0, fatol, xatol, maxfev, preds_scratch,
+                              speculate, spec_hits_out, g_ms_out, stream, true, &late);
+    if (rc != NNGP_OK && late)
+        rc = correction_sweep(sys, g_tableau, g_step_mode, g_steps, t, I, N, U1, UG1, UF, UG, model, X, Y, rows, m,
+                              n_jitter, jitter_exp_host, n_restarts, theta0, fatol, xatol, maxfev, preds_scratch,
+                              speculate, spec_hits_out, g_ms_out, stream, false, &late);
     return rc;
 }

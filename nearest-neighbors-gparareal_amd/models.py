@@ -132,6 +132,7 @@ class NNGP_p(ModelAbstr):
         self.train_count = 0
         self.k = 0
         self._dev_xy = None
+        self._host_xy = None
         if self.nn != 'adaptive' and not 1 <= int(self.nn) <= MAX_NEIGHBOURS:
             raise ValueError(f'nn={self.nn}: the GPU nnGP correction supports 1..{MAX_NEIGHBOURS} neighbours')
 
@@ -158,9 +159,24 @@ class NNGP_p(ModelAbstr):
         return out
 
     def fit(self, x, y, k, *args, **kwargs):
+        """models.py:157-159.  The Parareal driver hands over its device-resident training set
+        (torch tensors): those are kept for the device path, and `x` / `y` stay host arrays as in
+        the reference (copied from the device on first access)."""
         self.k = k
-        self.x, self.y = x, y
-        self._dev_xy = None
+        if hasattr(x, 'data_ptr'):
+            self._dev_xy = (x, y)
+            self._host_xy = None
+        else:
+            self._dev_xy = None
+            self._host_xy = (x, y)
+
+    def _host(self):
+        if self._host_xy is None:
+            self._host_xy = tuple(v.detach().cpu().numpy() for v in self._dev_xy)
+        return self._host_xy
+
+    x = property(lambda self: self._host()[0])
+    y = property(lambda self: self._host()[1])
 
     # ---------------------------------------------------------------------------- device path
     def predict_device(self, X, Y, rows, new_x, theta0, out=None, bias=None, preds=None,
@@ -186,8 +202,8 @@ class NNGP_p(ModelAbstr):
     def predict(self, new_x, prev_F=None, prev_G=None, *args, **kwargs):
         """models.py:171-183 (host arrays in/out; kNN + fits + argmin + mean on the GPU)."""
         torch = _lib.require_gpu()
-        if self._dev_xy is None:   # fit() may have been given host arrays or device tensors
-            self._dev_xy = (_lib.as_device(self.x), _lib.as_device(self.y))
+        if self._dev_xy is None:   # fit() was given host arrays
+            self._dev_xy = (_lib.as_device(self._host_xy[0]), _lib.as_device(self._host_xy[1]))
         X, Y = self._dev_xy
         q = torch.tensor(np.asarray(new_x, dtype=np.float64).reshape(-1), device='cuda')
         th0 = torch.tensor(self.draw_thetas(1), device='cuda')
@@ -261,9 +277,15 @@ class NNGP_p(ModelAbstr):
         return (*r['theta'][0], r['fval'][0], jitter, j, time.time() - st_)
 
     def store(self):
-        new = super().store()
+        """A deep copy for the result dict (models.py store): host x / y, no device tensors."""
+        if self._dev_xy is not None:
+            self._host()
+        dev, self._dev_xy = self._dev_xy, None
+        try:
+            new = super().store()
+        finally:
+            self._dev_xy = dev
         new.pool = None
-        new._dev_xy = None
         return new
 
     def state_dict(self):

@@ -21,11 +21,12 @@ import ctypes
 import json
 import os
 import time
+import warnings
 
 import numpy as np
 
 from . import _lib
-from .models import JITTERS, BareParareal, GPjax_p, NNGP_p
+from .models import JITTERS, MAX_NEIGHBOURS, BareParareal, GPjax_p, NNGP_p
 from .solver import SolverAbstr
 from .systems import ODE
 
@@ -215,6 +216,14 @@ class Parareal():
             mdl = BareParareal(N=self.N, **kwargs)
         elif model.lower() == 'nngp':
             mdl = NNGP_p(n=self.n, N=self.N, worker_pool=kwargs['pool'], **kwargs)
+            # nn='adaptive' grows m = k+2 (models.py:172-175); the GPU fits stop at m = 64, i.e. a
+            # run still unconverged after 63 iterations raises there.  Say so before any work.
+            es = kwargs.get('early_stop')
+            k_last = min(self.N, es if es is not None else self.N) - 1
+            if mdl.nn == 'adaptive' and max(10, k_last + 2) > MAX_NEIGHBOURS:
+                warnings.warn(f"nn='adaptive' with N={self.N}: iteration {MAX_NEIGHBOURS - 1} would need "
+                              f'm={MAX_NEIGHBOURS + 1} neighbours, beyond the GPU fits\' {MAX_NEIGHBOURS}; the run '
+                              f'raises if it gets there (pass early_stop <= {MAX_NEIGHBOURS - 1} or a fixed nn)')
         elif model.lower() == 'gpjax':
             mdl = GPjax_p(n=self.n, N=self.N, worker_pool=kwargs['pool'], **kwargs)
         elif model.lower() == 'elm':

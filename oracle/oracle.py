@@ -180,6 +180,27 @@ def paged(prop, t0, t1, steps, thresh, u0):
     return prop(t0, t1, steps, u0)
 
 
+def legacy_paged_batch(system, order, t0, t1, per_slice, thresh, U, nthreads=0):
+    """new_lib.RK_last (new_lib.py:57-69) over a batch of slices, on linspace grids: with
+    t_steps = per_slice + 1 points above RK_thresh, every page re-uses the full t_steps - 1 point
+    count over its sub-interval (float page lengths allowed).  Same float expressions as
+    nngp_amd.legacy.LegacySolverRK._rk_last."""
+    t0 = np.asarray(t0, dtype=float)
+    t1 = np.asarray(t1, dtype=float)
+    t_steps = int(per_slice) + 1
+    if not t_steps > thresh:
+        return system.rk_batch(order, t0, t1, t_steps - 1, U, STEP_LINSPACE, nthreads)
+    pts = t_steps - 1
+    iters = [thresh] * int(pts / thresh) + [pts % thresh] * (pts % thresh != 0)
+    step = (t1 - t0) / pts
+    t_s = t0
+    for temp in iters:
+        t_end = t_s + step * temp
+        U = system.rk_batch(order, t_s, t_end, pts - 1, U, STEP_LINSPACE, nthreads)
+        t_s = t_end
+    return U
+
+
 def d2_matrix(xm):
     xm = _c(xm)
     m, d = xm.shape
@@ -241,11 +262,13 @@ def predict(X, Y, q, m, theta0, n_restarts=1, fatol=0.1, xatol=0.1, maxfev=400, 
 # ---------------------------------------------------------------------------------------------
 def parareal(system, tspan, N, Ng, Nf, G, F, epsilon=5e-7, model='parareal', nn=10, seed=45,
              n_restarts=1, fatol=0.1, xatol=0.1, u0=None, step_mode=STEP_FIXED, nthreads=0,
-             early_stop=None, coarse_grid=False):
+             early_stop=None, coarse_grid=False, F_thresh=None, on_iter=None):
     """Returns dict(k, u, err, conv_int, converged, x, D) like Parareal._parareal.  Ng/Nf are
     per-slice step counts; coarse_grid=True takes the legacy initial coarse solution from one
     global grid of N*Ng steps (new_lib.py:902-906) -- with step_mode=STEP_LINSPACE this is the
-    legacy new_lib.Parareal loop (unpaged)."""
+    legacy new_lib.Parareal loop; F_thresh (with STEP_LINSPACE) adds RK_last's paging of the fine
+    solves (new_lib.py:57-69, 940-945).  on_iter(k, state) is called after every iteration
+    (progress reports of long runs)."""
     n = system.d
     order = {'RK1': 1, 'RK2': 2, 'RK4': 4, 'RK8': 8}
     oG, oF = order[G], order[F]
@@ -273,7 +296,11 @@ def parareal(system, tspan, N, Ng, Nf, G, F, epsilon=5e-7, model='parareal', nn=
     I = 0
     for k in range(N):
         U = u[I:N, :, k]
-        uF[I + 1:N + 1, :, k] = system.rk_batch(oF, t[I:N], t[I + 1:N + 1], Nf, U, step_mode, nthreads)
+        if F_thresh is not None:
+            assert step_mode == STEP_LINSPACE
+            uF[I + 1:N + 1, :, k] = legacy_paged_batch(system, oF, t[I:N], t[I + 1:N + 1], Nf, F_thresh, U, nthreads)
+        else:
+            uF[I + 1:N + 1, :, k] = system.rk_batch(oF, t[I:N], t[I + 1:N + 1], Nf, U, step_mode, nthreads)
         uG[I + 1, :, k + 1:] = uG[I + 1, :, k].reshape(-1, 1)      # parareal.py:331-333
         uF[I + 1, :, k + 1:] = uF[I + 1, :, k].reshape(-1, 1)
         u[I + 1, :, k + 1:] = uF[I + 1, :, k].reshape(-1, 1)
@@ -309,6 +336,8 @@ def parareal(system, tspan, N, Ng, Nf, G, F, epsilon=5e-7, model='parareal', nn=
             else:
                 break
         conv_int.append(I)
+        if on_iter is not None:
+            on_iter(k, {'I': I, 'u': u[:, :, :k + 2], 'err': err[:, :k + 1]})
         if I == N:
             break
         if early_stop is not None and k == early_stop - 1:

@@ -24,6 +24,18 @@ def run_case(g, case, shard):
         s = g.SolverRK(ode.get_vector_field(), Ng=5, Nf=100, F='RK8', G='RK4')
         p = g.Parareal(ode, s, [0, 8], 16, epsilon=5e-7, verbose=None)
         kw = dict(model='nngp', nn=20, seed=45, early_stop=2)
+    elif case == 'tomlab256':   # BASELINE configs[3]: N=256 (32 slices per rank on 8), configs.py schedule
+        from nngp_amd.configs import Config
+        ode = g.ThomasLabyrinth(normalization='-11')
+        cfg = Config(g.ThomasLabyrinth(normalization='-11'), N=256).get()
+        s = g.SolverRK(ode.get_vector_field(), Ng=cfg['Ng'], Nf=cfg['Nf'], F='RK4', G='RK1')
+        p = g.Parareal(ode, s, cfg['tspan'], 256, epsilon=5e-7, verbose=None)
+        kw = dict(model='nngp', nn=18, n_restarts=1, fatol=1e-3, xatol=1e-3, seed=45, early_stop=2)
+    elif case == 'fhn800':      # BASELINE configs[4]: FHN-PDE d=800 N=512 (64 slices, 100 coordinates per rank on 8)
+        ode = g.FHN_PDE(d_x=20)
+        s = g.SolverRK(ode.get_vector_field(), Ng=50, Nf=195325, F='RK8', G='RK4', thresh=float('inf'))
+        p = g.Parareal(ode, s, [0, 1100], 512, epsilon=5e-7, verbose=None)
+        kw = dict(model='nngp', nn=20, seed=45, early_stop=1)
     else:                   # classic Parareal on Lorenz (BASELINE configs[0]'s schedule)
         ode = g.Lorenz(normalization='-11')
         s = g.SolverRK(ode.get_vector_field(), Ng=6, Nf=450, F='RK4', G='RK4')

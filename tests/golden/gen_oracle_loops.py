@@ -1,0 +1,91 @@
+"""Oracle-loop fixtures for the published-scale parity tests (tests/test_gpu_published.py).
+
+Runs the CPU oracle's restatement of the Parareal loop (oracle/oracle.py `parareal`, OpenMP C
+kernels) on configurations too long to run on the GPU box inside the test suite, and commits
+the results as small fixtures: K, conv_int, the iterates of the first iterations, a SHA-256 of
+the whole iterate array and sampled rows.  The reference itself is not needed (or imported)
+here; the oracle is pinned to it by tests/test_oracle_golden.py.
+
+    python tests/golden/gen_oracle_loops.py burgers_pub_nngp_s45   # ~30 min on 8 cores
+    python tests/golden/gen_oracle_loops.py fhn800_n512_nngp       # ~15 min
+"""
+import hashlib
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+import oracle as O  # noqa: E402
+
+
+def u_digest(u):
+    """SHA-256 of the iterate array with NaNs canonicalised (the tests hash the GPU's the same way)."""
+    a = np.ascontiguousarray(np.nan_to_num(np.asarray(u, dtype=np.float64), nan=7.0))
+    return hashlib.sha256(a.tobytes()).hexdigest()
+
+
+def _progress(tag, t0):
+    def cb(k, st):
+        print(f'[{tag}] iteration {k + 1}: I={st["I"]} max err={np.nanmax(st["err"][:, -1]):.3e} '
+              f'({time.time() - t0:.0f} s)', flush=True)
+    return cb
+
+
+def burgers_pub(model, seed, nn=18):
+    """Burgers.py:27-122 (T=5): new_lib.Parareal with N=128, Ng=4N RK1, Nf=Ng*10^4 RK8 (TOTAL
+    steps), '-11' with bounds [0, 1], eps 5e-7, RK_thresh = Nf/N/200 -- 200 pages of 39 999 RK8
+    steps per slice per iteration, the legacy global coarse grid and linspace grids."""
+    N = 128
+    so = O.System('burgers', d=128, param=(0.01,), mn=0.0, mx=1.0)
+    x = np.linspace(-1, 1, 128)
+    u0 = so.fit(0.5 * (np.cos(4.5 * np.pi * x) + 1))
+    Ng, Nf = N * 4, N * 4 * 10000
+    thresh = Nf / N / 200
+    t0 = time.time()
+    kw = dict(model=model) if model == 'parareal' else dict(model=model, nn=nn, seed=seed)
+    o = O.parareal(so, [0, 5], N, Ng // N, Nf // N, 'RK1', 'RK8', epsilon=5e-7, u0=u0, step_mode=O.STEP_LINSPACE,
+                   coarse_grid=True, F_thresh=thresh, on_iter=_progress(f'burgers {model} {seed}', t0), **kw)
+    return o, time.time() - t0
+
+
+def fhn800(model='nngp'):
+    """BASELINE configs[4] (d_x = 20, d = 800, N = 512, T = 1100, no normalisation, u0 =
+    systems.py:303-312's seeded draw, nnGParareal m = 20, FHN_PDE.py:175) on FHN_PDE.py's 1e8 fine
+    schedule (Nf = ceil(1e8/12800)*12800 -> 195 325 RK8 steps per slice, FHN_PDE.py:54) with G =
+    RK4 50 steps per slice, run to convergence.  (configs.py:128-139's default branch, G = RK4
+    25/slice with F = RK8 25/slice, is unstable at d_x = 20: the oracle, like the reference's loop,
+    stops with 'NaN values in initial coarse solve' after the first iteration -- the GPU test
+    checks the same failure.)"""
+    so = O.System('fhn_pde', nx=20, normalized=False)
+    np.random.seed(45)
+    u0 = np.random.Generator(np.random.get_bit_generator()).uniform(size=800)
+    t0 = time.time()
+    o = O.parareal(so, [0, 1100], 512, 50, 195325, 'RK4', 'RK8', epsilon=5e-7, model=model, nn=20, seed=45, u0=u0,
+                   on_iter=_progress('fhn800', t0))
+    return o, time.time() - t0
+
+
+def main(which):
+    if which.startswith('burgers_pub'):
+        model = 'parareal' if 'para' in which.split('_')[2] else 'nngp'
+        seed = int(which.rsplit('_s', 1)[1]) if model == 'nngp' else 0
+        o, sec = burgers_pub(model, seed)
+        np.savez_compressed(os.path.join(HERE, f'{which}.npz'), k=o['k'], conv_int=np.array(o['conv_int']),
+                            converged=o['converged'], u3=o['u'][:, :, :3], digest=u_digest(o['u']),
+                            u_last=o['u'][:, :, -1], seconds=sec)
+    elif which == 'fhn800_n512_nngp':
+        o, sec = fhn800()
+        rows = np.array([0, 1, 2, 3, 128, 256, 384, 510, 511, 512])
+        np.savez_compressed(os.path.join(HERE, f'{which}.npz'), k=o['k'], conv_int=np.array(o['conv_int']),
+                            rows=rows, u_rows=o['u'][rows], digest=u_digest(o['u']), seconds=sec)
+    else:
+        raise SystemExit(f'unknown case {which}')
+    print(which, 'K', o['k'], 'conv_int', o['conv_int'], 'converged', o['converged'], f'{sec:.0f} s', flush=True)
+
+
+if __name__ == '__main__':
+    main(sys.argv[1])

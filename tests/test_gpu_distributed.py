@@ -1,5 +1,5 @@
 """Multi-rank orchestration WITH the HIP path (tests/test_distributed.py covers it on CPU with the
-oracle as propagator): 2 and 3 ranks in a gloo group share the box's one GPU (RCCL refuses
+oracle as propagator): 2, 3 and 8 ranks in a gloo group share the box's one GPU (RCCL refuses
 duplicate devices; gloo stages the all-gathers through host memory), each running the native
 kernels -- the fine sweep sharded into contiguous slice blocks and, for FHN-PDE, every
 prediction's fits sharded by coordinate (nngp_predict_range).  The iterates, K and conv_int must
@@ -24,9 +24,12 @@ def _port():
         return s.getsockname()[1]
 
 
+@pytest.mark.timeout(400)
 @pytest.mark.parametrize('case,shard,world', [('lorenz', 'none', 2), ('burgers', 'none', 2), ('burgers', '1', 3),
-                                              ('fhn', '1', 2)])
+                                              ('fhn', '1', 2), ('tomlab256', 'none', 8), ('fhn800', '1', 8)])
 def test_multi_rank_gpu_run_equals_single_rank(gpu, case, shard, world, tmp_path):
+    """world 8: BASELINE configs[3] / configs[4]'s 8-way partitions (TomLab N=256: 32 slices per
+    rank; FHN-PDE d=800 N=512: 64 slices and 100 of the 800 coordinates per rank)."""
     k1, conv1, u1 = run_case(gpu, case, None if shard == 'none' else shard == '1')
     out = str(tmp_path / 'rank0.npz')
     port = _port()
@@ -39,7 +42,7 @@ def test_multi_rank_gpu_run_equals_single_rank(gpu, case, shard, world, tmp_path
     logs = []
     for p in procs:
         try:
-            logs.append(p.communicate(timeout=240)[0].decode(errors='replace'))
+            logs.append(p.communicate(timeout=300)[0].decode(errors='replace'))
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()

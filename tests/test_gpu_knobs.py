@@ -1,0 +1,54 @@
+"""Every environment knob the HIP library reads (INTEGRATION.md "Knobs") selects another launch
+shape / kernel variant for the SAME arithmetic: each setting must leave a run bitwise unchanged
+(iterates, K, conv_int).  One small nnGParareal run per case, with and without the knob.
+
+The knobs are read on every call (csrc/common.h env_int), so monkeypatch toggles them in-process."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(gpu, case):
+    if case == 'burgers':     # d = 128 (wave propagator, LDS-staged kNN), 1 152 fits per prediction
+        ode = gpu.Burgers(d_x=128, normalization='-11')
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
+        p = gpu.Parareal(ode, s, [0, 1.25], 32, epsilon=5e-7, verbose=None)
+        kw = dict(model='nngp', nn=15, seed=45, early_stop=3)
+    elif case == 'fhn512':    # d = 512 (point-pair propagator, wave-per-pair D2), 4 608 fits (packed + park)
+        ode = gpu.FHN_PDE(d_x=16)
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=10, Nf=100, F='RK8', G='RK4')
+        p = gpu.Parareal(ode, s, [0, 4], 8, epsilon=5e-7, verbose=None)
+        kw = dict(model='nngp', nn=20, seed=45, early_stop=2)
+    else:                     # Lorenz (group / lane propagators), 27 fits per prediction
+        ode = gpu.Lorenz(normalization='-11')
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=6, Nf=450, F='RK4', G='RK4')
+        p = gpu.Parareal(ode, s, [0, 18], 32, epsilon=5e-7, verbose=None)
+        kw = dict(model='nngp', nn=10, seed=47)
+    r = p.run(**kw)
+    return r['k'], r['conv_int'], np.nan_to_num(r['u'], nan=7.0)
+
+
+_BASE = {}
+
+KNOBS = [
+    ('burgers', 'NNGP_NM_SPEC', '0'), ('burgers', 'NNGP_NM_SPEC', '1'), ('burgers', 'NNGP_NM_REFILL', '0'),
+    ('burgers', 'NNGP_NM_JMAJOR', '0'), ('burgers', 'NNGP_SPEC_OVERLAP', '0'), ('burgers', 'NNGP_RESPEC_W', '0'),
+    ('burgers', 'NNGP_RESPEC_W', '8'), ('burgers', 'NNGP_SPEC_MAX_FITS', '0'), ('burgers', 'NNGP_BURGERS_LDS', '1'),
+    ('burgers', 'NNGP_NM_PARK', '0'), ('burgers', 'NNGP_CHAIN', '1'), ('fhn512', 'NNGP_D2_WAVES', '0'),
+    ('fhn512', 'NNGP_FHN_PAIR', '0'), ('fhn512', 'NNGP_NM_PARK', '0'), ('fhn512', 'NNGP_NM_PARK', '20'),
+    ('fhn512', 'NNGP_RK_THREADS', '512'), ('lorenz', 'NNGP_RK_GROUP', '0'), ('lorenz', 'NNGP_CHAIN', '1'),
+]
+
+
+@pytest.mark.parametrize('case,knob,value', KNOBS)
+def test_knob_is_bitwise_neutral(gpu, case, knob, value, monkeypatch):
+    if case not in _BASE:
+        _BASE[case] = _run(gpu, case)
+    k0, c0, u0 = _BASE[case]
+    monkeypatch.setenv(knob, value)
+    if knob == 'NNGP_CHAIN':
+        monkeypatch.setenv('NNGP_CHAIN_PROF', '1')   # the chain's per-phase clocks must not change a bit either
+    k1, c1, u1 = _run(gpu, case)
+    assert (k1, c1) == (k0, c0)
+    assert np.array_equal(u1, u0)

@@ -51,10 +51,16 @@ def test_lorenz_nngp_k_distribution_matches_reference(gpu):
     assert np.mean(ks) <= 21
 
 
-def test_lorenz_nngp_bitwise_equals_oracle_loop(gpu):
+@pytest.mark.parametrize('chain', ['0', '1'])
+def test_lorenz_nngp_bitwise_equals_oracle_loop(gpu, chain, monkeypatch):
     """GPU kernels and the CPU oracle share every operation order (incl. exp/log/10^x), so even
-    the chaotic Lorenz nnGParareal run is reproduced bit for bit."""
+    the chaotic Lorenz nnGParareal run is reproduced bit for bit -- by the launch chain and by the
+    fused persistent chain (NNGP_CHAIN=1, §8f row 2), which must really run."""
+    from nngp_amd import _lib
+    monkeypatch.setenv('NNGP_CHAIN', chain)
+    n0, _ = _lib.chain_stats()
     r = _lorenz(gpu).run(model='nngp', nn=10, seed=45)
+    assert (_lib.chain_stats()[0] > n0) == (chain == '1')
     s = O.System('lorenz')
     o = O.parareal(s, [0, 18], 32, 6, 450, 'RK4', 'RK4', model='nngp', nn=10, seed=45, u0=s.fit([-15, -15, 20]))
     assert r['k'] == o['k'] and r['conv_int'] == o['conv_int']
@@ -215,12 +221,16 @@ def test_pararealight_returns_the_newest_iterate(gpu, model):
         gpu.PararealLight(ode, s, [0, 18], 32, verbose=None).run(model=model, store_int=True, **kw)
 
 
-@pytest.mark.parametrize('F', ['RK4', 'RK8'])
-def test_hopf_n128_nngp_bitwise_equals_oracle_loop(gpu, F):
+@pytest.mark.parametrize('F,chain', [('RK4', '0'), ('RK8', '0'), ('RK4', '1')])
+def test_hopf_n128_nngp_bitwise_equals_oracle_loop(gpu, F, chain, monkeypatch):
     """BASELINE configs[1], Hopf N=128 on the configs.py schedule (configs.py:35-46: Ng/N = 16 RK1,
     Nf/N = 1 360; F = RK4 as BASELINE names it, RK8 as configs.py has it) with Hopf.py's nnGP
     settings (nn=15, n_restarts=2, fatol=xatol=0.1, seed 45; Hopf.py:83-84): every iterate, K and
-    the converged-interval sequence equal the oracle's loop bit for bit (speculative sweep on)."""
+    the converged-interval sequence equal the oracle's loop bit for bit (speculative sweep on;
+    chain '1': the fused persistent chain, which must really run)."""
+    from nngp_amd import _lib
+    monkeypatch.setenv('NNGP_CHAIN', chain)
+    n0, _ = _lib.chain_stats()
     ode = gpu.Hopf(normalization='-11')
     s = gpu.SolverRK(ode.get_vector_field(), Ng=16, Nf=1360, F=F, G='RK1')
     kw = dict(nn=15, n_restarts=2, fatol=0.1, xatol=0.1, seed=45)
@@ -230,6 +240,7 @@ def test_hopf_n128_nngp_bitwise_equals_oracle_loop(gpu, F):
     print('Hopf N=128', F, 'K', r['k'], 'conv_int', r['conv_int'], 'spec hits', r['timings']['spec_hits'])
     assert r['converged'] and r['k'] == o['k'] and r['conv_int'] == o['conv_int']
     assert np.array_equal(np.nan_to_num(r['u'], nan=7.0), np.nan_to_num(o['u'], nan=7.0))
+    assert (_lib.chain_stats()[0] > n0) == (chain == '1')
 
 
 def _chain_case(gpu, case):
