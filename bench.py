@@ -600,16 +600,31 @@ def fhn_strong(torch, g, world, rank, steps=3, warmup=1, sample=400, n_pred=4):
 
 
 def read_traffic():
-    """HBM bytes per launch of the fine kernel from the committed PMC passes (tools/pmc_traffic.py:
-    the median over the profiled launches, with the max beside it)."""
-    path = os.path.join(ROOT, 'profiles', 'fine_kernel_traffic.json')
-    if os.path.exists(path):
-        try:
-            t = json.load(open(path))
-            return t.get('bytes_per_launch'), t.get('bytes_per_launch_max')
-        except Exception:
-            return None, None
-    return None, None
+    """HBM bytes per launch of the fine kernel from the NEWEST committed PMC passes
+    (profiles/rNN/fine_kernel_traffic.json, written by tools/pmc_traffic.py from rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of tools/pmc_probe.py): FETCH_SIZE x 2 (the guide's gfx950
+    correction) + WRITE_SIZE, median over the headline-length launches, every launch beside it,
+    and the same window's bytes under a null kernel (the device's background).  Returns
+    (summary dict, source path) or (None, None)."""
+    import glob
+    import re
+    cands = []
+    for p in glob.glob(os.path.join(ROOT, 'profiles', 'r[0-9]*', 'fine_kernel_traffic.json')):
+        m = re.search(r'r(\d+)', os.path.basename(os.path.dirname(p)))
+        cands.append((int(m.group(1)), p))
+    if not cands:
+        return None, None
+    path = max(cands)[1]
+    try:
+        t = json.load(open(path))
+    except Exception:
+        return None, None
+    if 'bytes_per_launch_all' not in t:   # pre-round-3 format (no x2 correction, no null kernel)
+        return None, None
+    return {'traffic': t['bytes_per_launch'], 'traffic_all_launches': t['bytes_per_launch_all'],
+            'traffic_short_launches': t.get('bytes_per_launch_short'),
+            'traffic_null_kernel_same_window': t.get('null_kernel_bytes_median'),
+            'traffic_correction': t.get('fetch_correction')}, os.path.relpath(path, ROOT)
 
 
 def main():
@@ -637,7 +652,8 @@ def main():
     value = total_steps / elapsed
     flops_launch = FLOPS_PER_STEP[('hopf', 'RK4')] * args.steps_per_slice * args.slices_per_gpu
     achieved_tf = flops_launch / kernel_s / 1e12
-    traffic, traffic_max = read_traffic()
+    tr, tr_src = read_traffic()
+    traffic = tr['traffic'] if tr else None
     res = {
         'metric': 'fine RK steps/sec (+ nnGP corrections/sec; wall-clock to convergence)',
         'value': value, 'unit': 'fine RK steps/s', 'n_gpus': world, 'steps': args.steps,
@@ -648,7 +664,7 @@ def main():
                    'steps_per_slice': args.steps_per_slice, 'parallelism': f'time-slices x{world}'},
         'roofline': {'bound': 'fp64-valu', 'achieved': achieved_tf, 'peak': FP64_PEAK_TFLOPS,
                      'unit': 'TFLOP/s', 'frac': achieved_tf / FP64_PEAK_TFLOPS, 'traffic': traffic,
-                     'traffic_max': traffic_max,
+                     **({k: v for k, v in tr.items() if k != 'traffic'} if tr else {}), 'traffic_source': tr_src,
                      'hbm_GBps': (traffic / kernel_s / 1e9) if traffic else None, 'hbm_peak_GBps': HBM_PEAK_GBS,
                      'algorithmic_bytes_per_launch': args.slices_per_gpu * (2 * 3 * 8 + 2 * 8),
                      'kernel': 'rk_group_kernel<HOPF,RK4>', 'kernel_ms': kernel_s * 1e3,

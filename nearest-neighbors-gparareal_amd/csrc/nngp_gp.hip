@@ -36,19 +36,14 @@
 
 #include "common.h"
 #include "nngp_math.h"
+#include "nngp_gpeval.h"
 #include "nngp_nm.h"
 #include "tableau.h"
 
 namespace nngp {
 
-static constexpr double LOG_2PI = 1.8378770664093453;   // np.log(2*np.pi)
 static constexpr int MAX_JIT = 16;
 
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // (value, index) order of numpy argsort with NaN last, on the squared distances the kNN selects
 // from (always >= +0 or NaN): the IEEE bit pattern of a non-negative double orders like its value,
@@ -743,364 +738,6 @@ __global__ void __launch_bounds__(256) d2_kernel(const double *__restrict__ xm, 
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// GP likelihood of one fit on ONE 16-lane DPP row
-//
-// A fit owns one row of a wave (lanes 16g .. 16g+15).  Lane l holds rows l and, for m > 16
-// (RPL = 2), l+16 of the m x m kernel matrix in VGPRs.  Every cross-lane move of the
-// factorisation is a broadcast of one lane to its row -- `v_mov_b64_dpp row_newbcast:L` on
-// gfx950, one VALU op, no LDS round trip -- and the two reductions are 4-level DPP butterflies.
-// The wave is VALU-issue-bound (tools/ubench_fp64.hip), so the design goal is the smallest
-// instruction count per likelihood evaluation:
-//   * K's lower triangle (m(m+1)/2 exps) is spread evenly over the 16 lanes (lane l builds
-//     entries l, l+16, ... of the flattened triangle, with their D2 values preloaded once per fit)
-//     and redistributed to the row owners through a small LDS image;
-//   * left-looking Cholesky with row broadcasts; forward solve with broadcasts; back solve from
-//     the transposed L read back from the same LDS image.
-// Arithmetic order (restated in oracle/nngp_oracle.c gp_factor / butterfly_sum):
-//   K_rj = psy*exp(c*D2_rj) (+ jit on the diagonal)                 models.py:146-155, 88
-//   L_ij = (K_ij - sum_k L_ik L_jk) * RN(1/L_jj), the sums in OpenBLAS dpotf2_L's order (ddot
-//          for the pivot, dgemv_n's 4-column fma blocks / tail-row fma chain below; gp_factor)
-//   z, alpha: successive subtraction, k ascending / descending; x/L_ii as Markstein x*RN(1/L_ii)
-//   sums over rows: lane pairs (l, l+16) first, then butterfly levels 1, 2, 4, 8
-// ---------------------------------------------------------------------------------------------
-template <int L>
-__device__ __forceinline__ double row_bcast(double v) {   // every lane <- lane L of its 16-row
-    return __builtin_amdgcn_mov_dpp(v, 0x150 + L, 0xF, 0xF, false);
-}
-
-template <int CTRL>
-__device__ __forceinline__ double dpp_mov(double v) {
-    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
-}
-
-// sum over the 16 lanes of a row, xor-butterfly order: quad_perm [1,0,3,2], quad_perm [2,3,0,1],
-// row_half_mirror, row_mirror.  After level s every lane of an aligned 2s-block holds the same
-// partial sum, so the mirrors deliver exactly the xor partner's value; a+b == b+a keeps every
-// lane bit-identical.
-__device__ __forceinline__ double row_sum(double v) {
-    v = v + dpp_mov<0xB1>(v);
-    v = v + dpp_mov<0x4E>(v);
-    v = v + dpp_mov<0x141>(v);
-    v = v + dpp_mov<0x140>(v);
-    return v;
-}
-
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for(F &&f) {
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        static_for<I + 1, N>(f);
-    }
-}
-
-// A fit of size m runs padded to MAXM (one of 8, 16, 20, 24, 32, 48, 64): rows m..MAXM-1 are
-// identity rows of K with y = 0.  The padded factorisation is exact -- L = [[L_m, 0], [0, I]], z
-// and alpha pad with exact zeros, every real row's arithmetic is untouched -- so every loop has a
-// compile-time trip count and no per-j branches.
-// MAXM <= 32 (one or two rows per lane): the triangle's exps are spread evenly over the 16 lanes
-// and redistributed through a full LDS image (stride S).  MAXM > 32 (m > 32: the adaptive
-// m = max(10, k+2) past k = 30, or an explicit nn, models.py:172-175): three or four rows per
-// lane, each lane builds its own rows' exps in registers (no redistribution), and the LDS image
-// is the PACKED lower triangle (row r at r(r+1)/2) that only the back solve reads -- a full image
-// would not fit four fits per workgroup in LDS at m = 64.
-template <int MAXM_> struct GP {
-    static constexpr int MAXM = MAXM_;
-    static constexpr int RPL = (MAXM + 15) / 16;                        // rows per lane
-    static constexpr bool BIG = MAXM > 32;
-    static constexpr int S = MAXM + 1;                                  // LDS row stride (pad)
-    static constexpr int IMG = BIG ? 8 * RPL * (16 * RPL + 1)           // image doubles / fit
-                                   : 16 * RPL * S;
-    static constexpr int NQ = BIG ? 1 : (MAXM * (MAXM + 1) / 2 + 15) / 16;   // triangle entries / lane
-};
-// LDS offset of K/L entry (r, j), j <= r, in a fit's image
-template <int MAXM>
-__device__ __forceinline__ int img_at(int r, int j) {
-    if constexpr (GP<MAXM>::BIG) return r * (r + 1) / 2 + j;
-    else return r * GP<MAXM>::S + j;
-}
-
-// per-lane, theta-independent part of a fit: where its share of the triangle lives
-// (idxq[q] = diagonal << 30 | D2 index << 16 | K-image slot; D2 index < 2^10, slot < 2^16)
-template <int MAXM> struct GPLane {
-    int idxq[GP<MAXM>::NQ];
-    int nq;           // entries this lane builds (<= NQ)
-};
-
-template <int MAXM>
-__device__ __forceinline__ void gp_lane_init(GPLane<MAXM> &P, int m, int l) {
-    constexpr int S = GP<MAXM>::S;
-    const int T = m * (m + 1) / 2;
-    P.nq = 0;
-    if constexpr (GP<MAXM>::BIG) return;   // rows are built by their owners (gp_factor)
-    int r = 0;
-#pragma unroll
-    for (int q = 0; q < GP<MAXM>::NQ; q++) {
-        const int t = l + 16 * q;
-        P.idxq[q] = 0;
-        if (t < T) {
-            while ((r + 1) * (r + 2) / 2 <= t) r++;
-            const int j = t - r * (r + 1) / 2;
-            P.idxq[q] = ((j == r) << 30) | ((r * m + j) << 16) | (r * S + j);
-            P.nq = q + 1;
-        }
-    }
-}
-
-// The fit's LDS image: rows >= m (the pad) are identity rows, written once per kernel and never
-// overwritten (the triangle build and the L write-back touch rows < m only).
-template <int MAXM>
-__device__ __forceinline__ void gp_image_init(double *Kimg, int m, int l) {
-    constexpr int RPL = GP<MAXM>::RPL, S = GP<MAXM>::S;
-    if constexpr (GP<MAXM>::BIG) {   // packed triangle: every pad-row entry (i >= m, j < i) is 0
-        for (int t = l; t < GP<MAXM>::IMG; t += 16) Kimg[t] = 0.0;
-        wave_lds_sync();
-        return;
-    }
-#pragma unroll
-    for (int s = 0; s < RPL; s++) {
-        const int row = l + 16 * s;
-#pragma unroll
-        for (int j = 0; j < MAXM; j++) Kimg[row * S + j] = (row >= m && j == row) ? 1.0 : 0.0;
-    }
-    wave_lds_sync();
-}
-
-// Factor K = psy*exp(c*D2) + jit*I and solve; returns false if potrf fails (jax: NaN).
-// alpha[s], diag[s] are those of row l + 16 s (meaningful for rows < m).
-template <int MAXM>
-__device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, const double *sD2,
-                                          double c, double psy, double jit,
-                                          const double (&y)[GP<MAXM>::RPL], double *Kimg,
-                                          double (&alpha)[GP<MAXM>::RPL],
-                                          double (&diag)[GP<MAXM>::RPL]) {
-    constexpr int RPL = GP<MAXM>::RPL, S = GP<MAXM>::S, NQ = GP<MAXM>::NQ;
-    double a[RPL][MAXM];
-    if constexpr (!GP<MAXM>::BIG) {
-        // 1) this lane's share of the triangle -> LDS image K[r*S + j]
-        wave_lds_sync();
-#pragma unroll
-        for (int q = 0; q < NQ; q++) {
-            if (q < P.nq) {
-                const int ix = P.idxq[q];
-                double e = psy * nn_exp(c * sD2[(ix >> 16) & 0x3FF]);    // k_gauss, models.py:146-148
-                if (ix >> 30) e = e + jit;                                // + eye*10**jitter, :88
-                Kimg[ix & 0xFFFF] = e;
-            }
-        }
-        wave_lds_sync();
-        // 2) own rows into registers (pad rows are the image's identity rows; the upper triangle
-        //    is never used)
-#pragma unroll
-        for (int s = 0; s < RPL; s++)
-#pragma unroll
-            for (int j = 0; j < MAXM; j++)
-                if (j < 16 * (s + 1)) a[s][j] = Kimg[(l + 16 * s) * S + j];
-    } else {
-        // 1+2) each lane builds its own rows (the same expressions, models.py:146-148, 88); pad
-        //      rows are identity rows, the upper triangle zeros (never used)
-#pragma unroll
-        for (int s = 0; s < RPL; s++) {
-            const int row = l + 16 * s;
-#pragma unroll
-            for (int j = 0; j < MAXM; j++) {
-                if (j >= 16 * (s + 1)) continue;
-                double e = (row >= m && j == row) ? 1.0 : 0.0;
-                if (row < m && j <= row) {
-                    e = psy * nn_exp(c * sD2[row * m + j]);
-                    if (j == row) e = e + jit;
-                }
-                a[s][j] = e;
-            }
-        }
-    }
-    // 3) left-looking Cholesky, row j broadcast from lane j%16 of set j/16.  The pivot is
-    //    broadcast, so every lane computes L_jj and RN(1/L_jj) identically; the row owner keeps
-    //    them.  Updates of rows < j (upper triangle) are computed and ignored: fewer
-    //    instructions than masking them.
-    bool fail = false;
-    double rinv[RPL];
-#pragma unroll
-    for (int s = 0; s < RPL; s++) {
-        diag[s] = 1.0;
-        rinv[s] = 1.0;
-    }
-    // OpenBLAS dpotf2_L's sums (the reference's LAPACK; oracle potf2_dot / potf2_gemv_row):
-    //   pivot   a_jj - ddot(row j): accumulators t1/t2 over groups of 4, fma(x0,x0,x2^2) etc.;
-    //   below   "vector rows" (the first ((m-1-j) & -4) rows under j): y -= 4-column fma chains,
-    //           leftover columns y -= a*x; "tail rows" (the last (m-1-j) & 3): y -= one fma chain.
-    //   Each lane evaluates both row forms (their operation counts add up to the old successive
-    //   subtraction's) and keeps the one its row takes.
-    // Once EVERY row of the wave has a failed pivot (each row is a fit, or a candidate of one
-    // fit), the -LML of all of them is +inf whatever follows: the remaining columns, both solves
-    // and the L write-back are skipped (a scalar branch per column).  Fits that wander where the
-    // kernel is singular for their jitter -- near-duplicate neighbours, FHN-PDE at its steady
-    // state -- evaluate +inf until maxfev (~8 % of a d = 800 correction's fits, the whole tail).
-    bool dead = false;   // wave-uniform
-    static_for<0, MAXM>([&](auto jc) {
-        constexpr int j = decltype(jc)::value, SJ = j / 16, LJ = j % 16;
-        if (dead) return;
-        const int tail_start = j + 1 + ((m - 1 - j) & ~3);
-        double yv[RPL], tt[RPL], blk[RPL];
-#pragma unroll
-        for (int s = 0; s < RPL; s++)
-            if (16 * (s + 1) > j) {
-                yv[s] = a[s][j];
-                tt[s] = 0.0;
-                blk[s] = 0.0;
-            }
-        double d1 = 0.0, d2 = 0.0;   // the pivot row's ddot (row j lives in set SJ, lane LJ)
-#pragma unroll
-        for (int k = 0; k < j; k++) {
-            const double ljk = row_bcast<LJ>(a[SJ][k]);
-#pragma unroll
-            for (int s = 0; s < RPL; s++)
-                if (16 * (s + 1) > j) {
-                    const double ak = a[s][k];
-                    if (k < (j & ~3)) {   // whole 4-column blocks of the vector-row form
-                        blk[s] = (k % 4 == 0) ? ak * ljk : fma(ak, ljk, blk[s]);
-                        if (k % 4 == 3) yv[s] = yv[s] - blk[s];
-                    } else {
-                        yv[s] = yv[s] - ak * ljk;
-                    }
-                    tt[s] = fma(ak, ljk, tt[s]);
-                }
-            // pivot ddot over the row-j owner's own entries L_jk (its set SJ)
-            const double xk = a[SJ][k];
-            if (k < (j & ~3)) {
-                if (k % 4 == 2) d1 = d1 + fma(a[SJ][k - 2], a[SJ][k - 2], xk * xk);
-                if (k % 4 == 3) d2 = d2 + fma(a[SJ][k - 2], a[SJ][k - 2], xk * xk);
-            } else {
-                d1 = fma(xk, xk, d1);
-            }
-        }
-        double t[RPL];
-#pragma unroll
-        for (int s = 0; s < RPL; s++)
-            if (16 * (s + 1) > j) t[s] = (l + 16 * s >= tail_start) ? a[s][j] - tt[s] : yv[s];
-        t[SJ] = (l == LJ) ? a[SJ][j] - (d1 + d2) : t[SJ];
-        const double piv = row_bcast<LJ>(t[SJ]);
-        fail = fail || !(piv > 0.0);
-        dead = __all(fail);
-        const double ljj = sqrt(piv);
-        const double ri = 1.0 / ljj;
-        diag[SJ] = (l == LJ) ? ljj : diag[SJ];
-        rinv[SJ] = (l == LJ) ? ri : rinv[SJ];
-#pragma unroll
-        for (int s = 0; s < RPL; s++)
-            if (16 * (s + 1) > j) a[s][j] = (l + 16 * s == j) ? ljj : t[s] * ri;
-    });
-    if (dead) {
-#pragma unroll
-        for (int s = 0; s < RPL; s++) alpha[s] = 0.0;
-        return false;
-    }
-    // x / L_ii for this lane's row of set s: Markstein-corrected x * RN(1/L_ii) (= IEEE x/L_ii)
-    auto divd = [&](int s, double x) {
-        const double q = x * rinv[s];
-        return fma(fma(-q, diag[s], x), rinv[s], q);
-    };
-    // 4) forward solve L z = y (models.py:90, inner solve_triangular); rows <= i update
-    //    harmlessly (their z is already captured)
-    double acc[RPL], z[RPL];
-#pragma unroll
-    for (int s = 0; s < RPL; s++) {
-        acc[s] = y[s];
-        z[s] = 0.0;
-    }
-    static_for<0, MAXM>([&](auto ic) {
-        constexpr int i = decltype(ic)::value, SI = i / 16, LI = i % 16;
-        const double zi = row_bcast<LI>(divd(SI, acc[SI]));
-        z[SI] = (l == LI) ? zi : z[SI];
-#pragma unroll
-        for (int s = 0; s < RPL; s++)
-            if (16 * (s + 1) > i + 1) acc[s] = acc[s] - a[s][i] * zi;
-    });
-    // 5) back solve L^T alpha = z: L to the LDS image, column of this lane's row(s) back
-    wave_lds_sync();
-#pragma unroll
-    for (int s = 0; s < RPL; s++) {
-        const int row = l + 16 * s;
-        if (row < m) {   // real rows only: the pad rows of the image stay identity (zero)
-#pragma unroll
-            for (int j = 0; j < MAXM; j++) {
-                if (j >= 16 * (s + 1)) continue;
-                if constexpr (GP<MAXM>::BIG) {
-                    if (j <= row) Kimg[img_at<MAXM>(row, j)] = a[s][j];
-                } else {
-                    Kimg[row * S + j] = a[s][j];
-                }
-            }
-        }
-    }
-    wave_lds_sync();
-    double acc2[RPL];
-#pragma unroll
-    for (int s = 0; s < RPL; s++) {
-        acc2[s] = z[s];
-        alpha[s] = 0.0;
-    }
-    static_for<0, MAXM>([&](auto ic) {
-        constexpr int i = MAXM - 1 - decltype(ic)::value, SI = i / 16, LI = i % 16;
-        const double ai = row_bcast<LI>(divd(SI, acc2[SI]));
-        alpha[SI] = (l == LI) ? ai : alpha[SI];
-#pragma unroll
-        for (int s = 0; s < RPL; s++)
-            if (16 * s < i) acc2[s] = acc2[s] - Kimg[img_at<MAXM>(i, l + 16 * s)] * ai;   // L[i][row]
-    });
-    return !fail;
-}
-
-// sum over the fit's rows r < m of v[r]: each lane adds its rows l, l+16, l+32, ... left to right
-// first, then the row butterfly (oracle butterfly_sum)
-template <int RPL>
-__device__ __forceinline__ double gp_rows_sum(int m, int l, const double (&v)[RPL]) {
-    double p = (l < m) ? v[0] : 0.0;
-#pragma unroll
-    for (int s = 1; s < RPL; s++) p = p + ((l + 16 * s < m) ? v[s] : 0.0);
-    return row_sum(p);
-}
-
-// -LML (models.py:240-252): NaN (incl. failed Cholesky) -> +inf
-template <int MAXM>
-__device__ __forceinline__ double gp_nlml(int m, int l, const GPLane<MAXM> &P, const double *sD2,
-                                          double sx, double sy,
-                                          double jit, const double (&y)[GP<MAXM>::RPL], double *Kimg) {
-    constexpr int RPL = GP<MAXM>::RPL;
-    const double c = -0.5 * (1 / nn_pow10(sx));
-    const double psy = nn_pow10(sy);
-    double alpha[RPL], diag[RPL], ya[RPL], lg[RPL];
-    const bool ok = gp_factor<MAXM>(m, l, P, sD2, c, psy, jit, y, Kimg, alpha, diag);
-#pragma unroll
-    for (int s = 0; s < RPL; s++) {
-        ya[s] = y[s] * alpha[s];
-        lg[s] = nn_log(diag[s]);
-    }
-    const double ydot = gp_rows_sum<RPL>(m, l, ya);
-    const double slog = gp_rows_sum<RPL>(m, l, lg);
-    const double res = -(((-0.5 * ydot) - slog) - ((double)m / 2) * LOG_2PI);
-    return (!ok || res != res) ? INFINITY : res;
-}
-
-// posterior mean K(xm, new_x)^T alpha (models.py:162-168); NaN on Cholesky failure
-template <int MAXM>
-__device__ __forceinline__ double gp_mean(int m, int l, const GPLane<MAXM> &P, const double *sD2,
-                                          const double *skd2,
-                                          double sx, double sy, double jit,
-                                          const double (&y)[GP<MAXM>::RPL], double *Kimg) {
-    constexpr int RPL = GP<MAXM>::RPL;
-    const double c = -0.5 * (1 / nn_pow10(sx));
-    const double psy = nn_pow10(sy);
-    double alpha[RPL], diag[RPL], ka[RPL];
-    const bool ok = gp_factor<MAXM>(m, l, P, sD2, c, psy, jit, y, Kimg, alpha, diag);
-#pragma unroll
-    for (int s = 0; s < RPL; s++) {
-        const int row = l + 16 * s;
-        ka[s] = (psy * nn_exp(c * skd2[row < m ? row : 0])) * alpha[s];
-    }
-    const double mean = gp_rows_sum<RPL>(m, l, ka);
-    return ok ? mean : NAN;
-}
 
 // Nelder-Mead state machine: nngp_nm.h
 

@@ -148,6 +148,45 @@ __device__ __forceinline__ void nn_sincos(double x, double &sn, double &cs) {
     cs = fin ? c_ : nanv;
 }
 
+// sin alone (ThomasLabyrinth, systems.py:257-271, whose three sines are all it evaluates): x = n pi
+// + r by the same three-term fma reduction (fdlibm's 33-bit pieces, doubled), |r| <= pi/2, then ONE
+// odd polynomial r + r^3 P(r^2) (8 coefficients, a weighted minimax fit of sin(r)/r - 1 on
+// [0, (pi/2)^2] computed with mpmath, relative error 2.8e-19; tests/golden/sin_pi_fit.py) and the
+// sign (-1)^n as a sign-bit xor.  No quadrant select between two polynomials, so ~20 VALU
+// instead of ~40 per sine.  <= 2 ulp from glibc (tests/test_oracle_golden.py).
+struct SinPiC {
+    static constexpr double INVPI = 0x1.45f306dc9c883p-2;
+    static constexpr double PI_1 = 2 * 1.57079632673412561417e+00, PI_2 = 2 * 6.07710050630396597660e-11,
+                            PI_3 = 2 * 2.02226624871116645580e-21;
+    static constexpr double S1 = -0x1.5555555555555p-3, S2 = 0x1.11111111110c1p-7, S3 = -0x1.a01a01a0148bbp-13,
+                            S4 = 0x1.71de3a5287c12p-19, S5 = -0x1.ae6454cb54cccp-26, S6 = 0x1.6123cb28741dap-33,
+                            S7 = -0x1.ae431d76c3814p-41, S8 = 0x1.88299fb2db5f9p-49;
+};
+
+__device__ __forceinline__ double nn_sin_pi(double x) {
+    const double n = rint(x * SinPiC::INVPI);
+    double r = fma(-n, SinPiC::PI_1, x);
+    r = fma(-n, SinPiC::PI_2, r);
+    r = fma(-n, SinPiC::PI_3, r);
+    const double z = r * r;
+    double p = fma(SinPiC::S8, z, SinPiC::S7);
+    p = fma(p, z, SinPiC::S6);
+    p = fma(p, z, SinPiC::S5);
+    p = fma(p, z, SinPiC::S4);
+    p = fma(p, z, SinPiC::S3);
+    p = fma(p, z, SinPiC::S2);
+    p = fma(p, z, SinPiC::S1);
+    const double s = fma(r * z, p, r);
+    // (-1)^n: the low bit of n + 1.5*2^52 (n in two's complement for |n| < 2^51), into the sign
+    const long long par = __double_as_longlong(n + 6755399441055744.0) & 1;
+    const double sg = __longlong_as_double(__double_as_longlong(s) ^ (par << 63));
+#ifdef NNGP_RK_FMA
+    return sg;   // contracted build: inf/NaN already give NaN (r = NaN)
+#else
+    return (x - x == 0.0) ? sg : x - x;   // NaN for inf / NaN arguments, as sin
+#endif
+}
+
 __device__ __forceinline__ double nn_sin(double x) {
     double s, c;
     nn_sincos(x, s, c);

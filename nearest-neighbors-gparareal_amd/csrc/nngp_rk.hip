@@ -125,7 +125,7 @@ template <> struct GroupSys<NNGP_SYS_HOPF> {     // systems.py:148-154, as LaneS
 template <> struct GroupSys<NNGP_SYS_THOMAS_LABYRINTH> {   // systems.py:257-271
     static constexpr int G = 4;
     __device__ static double f(double x, int, double, const LaneArgs &) {
-        const double sn = quad_mov<QROT>(nn_sin(x));   // sin(u[c+1 mod 3])
+        const double sn = quad_mov<QROT>(nn_sin_pi(x));   // sin(u[c+1 mod 3])
         return -0.5 * x + 10.0 * sn;
     }
 };

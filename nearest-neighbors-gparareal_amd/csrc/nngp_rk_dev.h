@@ -46,9 +46,9 @@ template <> struct LaneSys<NNGP_SYS_HOPF> {     // systems.py:148-154
 template <> struct LaneSys<NNGP_SYS_THOMAS_LABYRINTH> {   // systems.py:257-271
     static constexpr int D = 3;
     __device__ static void f(const double *u, double *o, const LaneArgs &) {
-        o[0] = -0.5 * u[0] + 10.0 * nn_sin(u[1]);
-        o[1] = -0.5 * u[1] + 10.0 * nn_sin(u[2]);
-        o[2] = -0.5 * u[2] + 10.0 * nn_sin(u[0]);
+        o[0] = -0.5 * u[0] + 10.0 * nn_sin_pi(u[1]);
+        o[1] = -0.5 * u[1] + 10.0 * nn_sin_pi(u[2]);
+        o[2] = -0.5 * u[2] + 10.0 * nn_sin_pi(u[0]);
     }
 };
 template <> struct LaneSys<NNGP_SYS_FHN_ODE> {  // systems.py:87-95 (u**3 = u*(u*u), jax)

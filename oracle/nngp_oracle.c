@@ -59,6 +59,7 @@ typedef struct {
 /* fully specified sin/cos (defined below, restating csrc/nngp_math.h) */
 void nn_sincos(double x, double *sn, double *cs);
 double nn_sin(double x);
+double nn_sin_pi(double x);
 double nn_cos(double x);
 
 static void make_tableau(int order, tableau_t *T) {
@@ -315,9 +316,9 @@ static void rhs_raw(const nngp_system *sys, const double *u, double *out) {
     }
     case NNGP_SYS_THOMAS_LABYRINTH: {
         const double a = 0.5, b = 10.0;
-        out[0] = -a * u[0] + b * nn_sin(u[1]);
-        out[1] = -a * u[1] + b * nn_sin(u[2]);
-        out[2] = -a * u[2] + b * nn_sin(u[0]);
+        out[0] = -a * u[0] + b * nn_sin_pi(u[1]);
+        out[1] = -a * u[1] + b * nn_sin_pi(u[2]);
+        out[2] = -a * u[2] + b * nn_sin_pi(u[0]);
         break;
     }
     case NNGP_SYS_FHN_ODE: {
@@ -622,6 +623,39 @@ void nn_sincos(double x, double *sn, double *cs) {
     const double nanv = x - x;
     *sn = fin ? s_ : nanv;
     *cs = fin ? c_ : nanv;
+}
+
+/* sin alone, restating csrc/nngp_math.h nn_sin_pi bit for bit (ThomasLabyrinth): x = n pi + r,
+ * |r| <= pi/2, one odd polynomial, sign (-1)^n. */
+static const double SP_INVPI = 0x1.45f306dc9c883p-2;
+static const double SP_PI_1 = 2 * 1.57079632673412561417e+00, SP_PI_2 = 2 * 6.07710050630396597660e-11,
+                    SP_PI_3 = 2 * 2.02226624871116645580e-21;
+static const double SP_S1 = -0x1.5555555555555p-3, SP_S2 = 0x1.11111111110c1p-7, SP_S3 = -0x1.a01a01a0148bbp-13,
+                    SP_S4 = 0x1.71de3a5287c12p-19, SP_S5 = -0x1.ae6454cb54cccp-26, SP_S6 = 0x1.6123cb28741dap-33,
+                    SP_S7 = -0x1.ae431d76c3814p-41, SP_S8 = 0x1.88299fb2db5f9p-49;
+
+double nn_sin_pi(double x) {
+    const int fin = (x - x) == 0.0;
+    const double n = rint(x * SP_INVPI);
+    double r = fma(-n, SP_PI_1, x);
+    r = fma(-n, SP_PI_2, r);
+    r = fma(-n, SP_PI_3, r);
+    const double z = r * r;
+    double p = fma(SP_S8, z, SP_S7);
+    p = fma(p, z, SP_S6);
+    p = fma(p, z, SP_S5);
+    p = fma(p, z, SP_S4);
+    p = fma(p, z, SP_S3);
+    p = fma(p, z, SP_S2);
+    p = fma(p, z, SP_S1);
+    double s = fma(r * z, p, r);
+    const double nq = n + 6755399441055744.0;
+    uint64_t nb, sb;
+    memcpy(&nb, &nq, sizeof nb);
+    memcpy(&sb, &s, sizeof sb);
+    sb ^= (nb & 1u) << 63;
+    memcpy(&s, &sb, sizeof s);
+    return fin ? s : x - x;
 }
 
 double nn_sin(double x) {

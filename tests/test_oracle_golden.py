@@ -99,11 +99,17 @@ def test_math_accuracy():
     assert np.max(np.abs(got - np.log(ls)) / np.spacing(np.abs(np.log(ls)))) <= 2
     assert L.nn_log(0.0) == -np.inf and np.isnan(L.nn_log(-1.0))
     xs = np.concatenate([rng.uniform(-40, 40, 20000), rng.uniform(-1e4, 1e4, 2000), [0.0, np.pi / 2, -np.pi]])
-    for fn, ref in (('nn_sin', np.sin), ('nn_cos', np.cos)):
+    for fn, ref in (('nn_sin', np.sin), ('nn_cos', np.cos), ('nn_sin_pi', np.sin)):
         got = np.array([getattr(L, fn)(x) for x in xs])
         r = ref(xs)
         assert np.max(np.abs(got - r) / np.maximum(np.spacing(np.abs(r)), np.spacing(1.0) * 2 ** -10)) <= 2, fn
     assert np.isnan(L.nn_sin(np.inf)) and np.isnan(L.nn_cos(np.nan))
+    assert np.isnan(L.nn_sin_pi(np.inf)) and np.isnan(L.nn_sin_pi(-np.inf)) and np.isnan(L.nn_sin_pi(np.nan))
+    # the pi-reduced sine at 200k points of ThomasLabyrinth's range (|x| <= 15) and at +-0
+    xs = rng.uniform(-15, 15, 200000)
+    got = np.array([L.nn_sin_pi(x) for x in xs])
+    assert np.max(np.abs(got - np.sin(xs)) / np.maximum(np.spacing(np.abs(np.sin(xs))), 2.0 ** -1074)) <= 2
+    assert L.nn_sin_pi(0.0) == 0.0 and L.nn_sin_pi(1e-300) == 1e-300   # (the sign of a zero is not kept)
 
 
 def test_nlml_matches_reference():
