@@ -46,6 +46,12 @@ def main():
     rate = 100_000_000 / (time.perf_counter() - a)
     cycles = int(min(dur, 5.0) * rate)
     print(f'long launch {dur:.3f} s; null kernel {rate:.3e} cycles/s -> {cycles} cycles', flush=True)
+    if len(sys.argv) > 2 and sys.argv[1] == 'null':   # many null windows only (the background's rate)
+        for i in range(int(sys.argv[2])):
+            torch.cuda._sleep(cycles)
+            torch.cuda.synchronize()
+        print('done', flush=True)
+        return
     for i in range(4):
         solver_long.run_F_batch(t0, t1, u0, out=out)
         torch.cuda.synchronize()
