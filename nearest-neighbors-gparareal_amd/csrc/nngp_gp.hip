@@ -1001,6 +1001,17 @@ __device__ __forceinline__ int nm_candidates(const NM &S, NMCand (&c)[4]) {
         c[2] = NMCand{S.s2x, S.s2y, ST_INIT2};
         return 3;
     case ST_REFLECT:   // same expressions as nm_consume's ST_REFLECT branch
+        if (S.f0 == INFINITY && S.f1 == INFINITY && S.f2 == INFINITY) {
+            // an all-+inf simplex (the jittered kernel fails the Cholesky at every vertex so far;
+            // ~8 % of an FHN-PDE d = 800 correction's fits, which then run to maxfev): if the
+            // reflection is +inf too, scipy takes the inside contraction (fxr >= f2), and if that
+            // is +inf the shrink's two points -- one iteration in ONE round instead of two.  A finite
+            // reflection takes the expansion instead, answered in the next round as before.
+            c[1] = NMCand{0.5 * S.xbx + 0.5 * S.s2x, 0.5 * S.xby + 0.5 * S.s2y, ST_ICONTRACT};
+            c[2] = NMCand{S.s0x + 0.5 * (S.s1x - S.s0x), S.s0y + 0.5 * (S.s1y - S.s0y), ST_SHRINK1};
+            c[3] = NMCand{S.s0x + 0.5 * (S.s2x - S.s0x), S.s0y + 0.5 * (S.s2y - S.s0y), ST_SHRINK2};
+            return 4;
+        }
         c[1] = NMCand{3 * S.xbx - 2 * S.s2x, 3 * S.xby - 2 * S.s2y, ST_EXPAND};
         c[2] = NMCand{1.5 * S.xbx - 0.5 * S.s2x, 1.5 * S.xby - 0.5 * S.s2y, ST_CONTRACT};
         c[3] = NMCand{0.5 * S.xbx + 0.5 * S.s2x, 0.5 * S.xby + 0.5 * S.s2y, ST_ICONTRACT};

@@ -973,9 +973,16 @@ typedef struct {
     double jit;
 } nlml_ctx_t;
 
+/* Roundoff-sensitivity experiment only (tests/golden/gen_oracle_loops.py *_lmlscale): every
+ * Nelder-Mead objective value is multiplied by this factor -- 1 + 2^-52 is a one-ulp relative
+ * perturbation of the -LML, the size of the difference between two libms or BLAS orders.  The
+ * default 1.0 leaves the oracle exact (x * 1.0 == x). */
+static double g_lml_scale = 1.0;
+void orc_set_lml_scale(double s) { g_lml_scale = s; }
+
 static double nlml_fn(const double *x, void *vctx) {
     const nlml_ctx_t *c = (const nlml_ctx_t *)vctx;
-    return orc_nlml(c->m, c->D2, c->y, x[0], x[1], c->jit);
+    return orc_nlml(c->m, c->D2, c->y, x[0], x[1], c->jit) * g_lml_scale;
 }
 
 /* one hyper-parameter fit: NNGP_p._get_opt_par / opt_theta (models.py:228-260)              */
