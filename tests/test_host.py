@@ -186,3 +186,41 @@ def test_nngp_neighbour_bound_is_explicit():
     ad.k = 63
     with pytest.raises(ValueError, match='adaptive'):
         ad.n_neighbours()
+
+
+def test_bench_roofline_traffic_is_the_committed_pmc_figure():
+    """bench.py's roofline.traffic comes from the newest committed PMC record (profiles/rNN/
+    fine_kernel_traffic.json, tools/pmc_traffic.py): FETCH_SIZE x 2 + WRITE_SIZE, median over the
+    headline-length launches, with every launch listed."""
+    import json
+    import os
+    import statistics
+    import bench
+    tr, src = bench.read_traffic()
+    assert tr is not None and src.startswith('profiles/r')
+    rec = json.load(open(os.path.join(os.path.dirname(bench.__file__), src)))
+    fetch = [d['bytes'] for d in rec['dispatches_fetch_pass'] if d['class'] == 'fine_long']
+    write = [d['bytes'] for d in rec['dispatches_write_pass'] if d['class'] == 'fine_long']
+    raw = [d['fetch_size_raw_bytes'] for d in rec['dispatches_fetch_pass'] if d['class'] == 'fine_long']
+    assert fetch == [2 * r for r in raw]                 # the guide's gfx950 FETCH_SIZE correction
+    assert tr['traffic'] == statistics.median(fetch) + statistics.median(write)
+    assert len(tr['traffic_all_launches']) == len(fetch)
+
+
+def test_adaptive_nn_warns_up_front_when_n_could_outgrow_the_fits(monkeypatch):
+    """nn='adaptive' (m = k+2) past 63 iterations exceeds the GPU fits' m <= 64: Parareal.run says
+    so before any work (the run itself raises only if it gets there)."""
+    import warnings
+    import nngp_amd as g
+    ode = g.Lorenz(normalization='-11')
+    s = g.SolverRK(ode.get_vector_field(), Ng=6, Nf=450, F='RK4', G='RK4')
+    p = g.Parareal(ode, s, [0, 18], 80, verbose=None)
+    monkeypatch.setattr(p, '_parareal', lambda mdl, **kw: {'timings': {}})
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter('always')
+        p.run(model='nngp', nn='adaptive')
+    assert any('adaptive' in str(x.message) for x in w)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter('always')
+        p.run(model='nngp', nn='adaptive', early_stop=40)
+    assert not any('adaptive' in str(x.message) for x in w)
