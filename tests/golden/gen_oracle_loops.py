@@ -9,6 +9,7 @@ here; the oracle is pinned to it by tests/test_oracle_golden.py.
     python tests/golden/gen_oracle_loops.py burgers_pub_nngp_s45   # ~30 min on 8 cores
     python tests/golden/gen_oracle_loops.py fhn800_n512_nngp       # ~15 min
     python tests/golden/gen_oracle_loops.py burgers_pub_nngp_s45_lmlscale   # K's roundoff sensitivity
+    python tests/golden/gen_oracle_loops.py tomlab256_nngp         # TomLab N=256 to convergence
 """
 import hashlib
 import os
@@ -70,6 +71,18 @@ def fhn800(model='nngp'):
     return o, time.time() - t0
 
 
+def tomlab256():
+    """BASELINE configs[3]'s size to convergence: ThomasLabyrinth N=256 on configs.py's schedule
+    (T = 100, G = RK1 10 / F = RK4 3 910 steps per slice) with TomLab.py's nnGP settings (nn = 18,
+    fatol = xatol = 1e-3, seed 45), '-11' normalisation, u0 as systems.py:253."""
+    so = O.System('tomlab')
+    t0 = time.time()
+    o = O.parareal(so, [0, 100], 256, 10, 3910, 'RK1', 'RK4', epsilon=5e-7, model='nngp', nn=18, seed=45,
+                   fatol=1e-3, xatol=1e-3, u0=so.fit([4.6722764, 5.2437205e-10, -6.4444208e-10]),
+                   on_iter=None)
+    return o, time.time() - t0
+
+
 def main(which):
     if which.startswith('burgers_pub') and 'lmlscale' in which:
         # roundoff sensitivity of K on the published schedule: the same run with every -LML the
@@ -85,6 +98,10 @@ def main(which):
         np.savez_compressed(os.path.join(HERE, f'{which}.npz'), k=o['k'], conv_int=np.array(o['conv_int']),
                             converged=o['converged'], u3=o['u'][:, :, :3], digest=u_digest(o['u']),
                             u_last=o['u'][:, :, -1], seconds=sec)
+    elif which == 'tomlab256_nngp':
+        o, sec = tomlab256()
+        np.savez_compressed(os.path.join(HERE, f'{which}.npz'), k=o['k'], conv_int=np.array(o['conv_int']),
+                            converged=o['converged'], digest=u_digest(o['u']), u_last=o['u'][:, :, -1], seconds=sec)
     elif which == 'fhn800_n512_nngp':
         o, sec = fhn800()
         rows = np.array([0, 1, 2, 3, 128, 256, 384, 510, 511, 512])

@@ -5,8 +5,9 @@ It is NOT bitwise the reference's rounding order, so it is held to a stated tole
   * per-slice end states within 1e-12 relative (max |a - b| / max(1, max |b|)) of the exact
     build / the CPU oracle on every fixture system, tableau and step convention;
   * the same converged iteration count K as the exact build on Lorenz Parareal (N=32), FHN-ODE
-    Parareal and nnGParareal (N=40), and Burgers nnGParareal (N=128, m=15) -- the configurations
-    whose K the exact build matches to the reference.
+    Parareal and nnGParareal (N=40), Burgers nnGParareal (N=128, m=15), Hopf nnGParareal (N=128,
+    configs.py) and TomLab nnGParareal (N=32, configs.py);
+  * and where it does NOT keep K, the pinned pair: TomLab N=256 (exact 162, contracted 150).
 The exact build stays the default (tests/test_gpu_kernels.py pins it bit for bit)."""
 import numpy as np
 import pytest
@@ -75,9 +76,20 @@ def _k(gpu, ode, tspan, N, Ng, Nf, F, G, fma, **run):
     return r['k'], list(r['conv_int'])
 
 
-@pytest.mark.parametrize('case', ['lorenz_parareal', 'fhn_ode_parareal', 'fhn_ode_nngp', 'burgers_nngp'])
+@pytest.mark.parametrize('case', ['lorenz_parareal', 'fhn_ode_parareal', 'fhn_ode_nngp', 'burgers_nngp', 'hopf_nngp',
+                                  'tomlab32_nngp'])
 def test_contracted_run_keeps_k(gpu, case):
-    if case == 'lorenz_parareal':
+    """hopf_nngp: configs.py's Hopf N=128 (RK8 1 360 / RK1 16 per slice) with Hopf.py's nnGP settings
+    (nn=15, R=2): K = 14 in both builds; tomlab32_nngp: configs.py's TomLab N=32 (RK4 31 250 / RK1 10,
+    T = 10) with TomLab.py's (nn=18, fatol=xatol=1e-3): K = 25 in both (tools/contract_k_probe.py,
+    profiles/r03/contract_k.txt)."""
+    if case == 'hopf_nngp':
+        args = (gpu.Hopf(normalization='-11'), [-20, 500], 128, 16, 1360, 'RK8', 'RK1')
+        run = dict(model='nngp', nn=15, n_restarts=2, fatol=0.1, xatol=0.1, seed=45)
+    elif case == 'tomlab32_nngp':
+        args = (gpu.ThomasLabyrinth(normalization='-11'), [0, 10], 32, 10, 31250, 'RK4', 'RK1')
+        run = dict(model='nngp', nn=18, fatol=1e-3, xatol=1e-3, seed=45)
+    elif case == 'lorenz_parareal':
         args = (gpu.Lorenz(normalization='-11'), [0, 18], 32, 6, 450, 'RK4', 'RK4')
         run = dict(model='parareal')
     elif case.startswith('fhn_ode'):   # test_gpu_parareal.test_fhn_ode_matches_reference's config
@@ -91,3 +103,20 @@ def test_contracted_run_keeps_k(gpu, case):
     k_fm, c_fm = _k(gpu, ode, tspan, N, Ng, Nf, F, G, True, **run)
     print(case, 'exact K', k_ex, 'contracted K', k_fm)
     assert k_fm == k_ex
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(300)
+def test_contracted_build_changes_k_on_tomlab_n256(gpu):
+    """The contracted build is NOT K-preserving everywhere: TomLab N=256 on configs.py's schedule
+    (RK4 3 910 / RK1 10 per slice, T = 100; TomLab.py's nnGP settings) converges in K = 162 with
+    the exact build (the oracle loop's K, tests/golden/tomlab256_nngp.npz when present) and in
+    K = 150 with the contracted one -- a chaotic field over 150+ iterations.  Pinned so that no
+    published-schedule ratio is quoted for the contracted build as if K were unchanged (DESIGN.md
+    §3.1c); the exact build already beats the reference's TomLab cluster per iteration."""
+    args = (gpu.ThomasLabyrinth(normalization='-11'), [0, 100], 256, 10, 3910, 'RK4', 'RK1')
+    run = dict(model='nngp', nn=18, fatol=1e-3, xatol=1e-3, seed=45)
+    k_ex, _ = _k(gpu, *args, False, **run)
+    k_fm, _ = _k(gpu, *args, True, **run)
+    print('tomlab N=256 exact K', k_ex, 'contracted K', k_fm)
+    assert (k_ex, k_fm) == (162, 150)
