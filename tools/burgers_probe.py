@@ -18,7 +18,11 @@ def run(early_stop=None):
     p = g.Parareal(ode, solver, [0, 5], 128, epsilon=5e-7, verbose=None)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    r = p.run(model='nngp', nn=15, seed=45, early_stop=early_stop)
+    if os.environ.get('NNGP_PROBE_STREAM') == '1':   # the run on a non-default stream
+        with torch.cuda.stream(torch.cuda.Stream()):
+            r = p.run(model='nngp', nn=15, seed=45, early_stop=early_stop)
+    else:
+        r = p.run(model='nngp', nn=15, seed=45, early_stop=early_stop)
     torch.cuda.synchronize()
     return time.perf_counter() - t0, r
 
