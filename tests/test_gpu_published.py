@@ -133,3 +133,22 @@ def test_fhn_pde_d800_default_branch_raises_like_the_reference(gpu):
     assert (cfg['Ng'], cfg['Nf'], cfg['tspan'], cfg['G'], cfg['F']) == (25, 25, [0, 1100], 'RK4', 'RK8')
     with pytest.raises(Exception, match='NaN values in initial coarse solve'):
         fhn800_n512(gpu, cfg['Ng'], cfg['Nf']).run(model='nngp', nn=20, seed=45)
+
+
+@pytest.mark.timeout(300)
+def test_tomlab_n256_nngp_to_convergence_bitwise_oracle_loop(gpu):
+    """BASELINE configs[3]'s size to convergence: ThomasLabyrinth N=256 on configs.py's schedule
+    (configs.py:50-57: T=100, Ng/N=10 RK1, Nf/N=3 910 RK4) with TomLab.py's nnGP settings (nn=18,
+    fatol=xatol=1e-3, seed 45): K = 162 and every iterate of the 162 iterations bitwise the
+    oracle loop's (tests/golden/tomlab256_nngp.npz; the published run on the 1e9 schedule: K = 159)."""
+    from nngp_amd.configs import Config
+    P = golden('tomlab256_nngp.npz')
+    ode = gpu.ThomasLabyrinth(normalization='-11')
+    cfg = Config(gpu.ThomasLabyrinth(normalization='-11'), N=256).get()
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=cfg['Ng'], Nf=cfg['Nf'], F='RK4', G='RK1')
+    r = gpu.Parareal(ode, s, cfg['tspan'], 256, epsilon=5e-7, verbose=None).run(
+        model='nngp', nn=18, n_restarts=1, fatol=1e-3, xatol=1e-3, seed=45)
+    print(f"TomLab N=256 to convergence: K={r['k']} (oracle {int(P['k'])}) runtime={r['timings']['runtime']:.1f}s")
+    assert r['k'] == int(P['k']) and r['conv_int'] == list(P['conv_int'])
+    assert np.array_equal(np.nan_to_num(r['u'][:, :, -1], nan=7.0), np.nan_to_num(P['u_last'], nan=7.0))
+    assert u_digest(r['u']) == str(P['digest'])
