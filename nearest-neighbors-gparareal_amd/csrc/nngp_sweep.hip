@@ -70,22 +70,7 @@ static int respec_resources(size_t nflags, Respec **out) {
         NNGP_HIP_CHECK(hipStreamCreateWithFlags(&r.st2, hipStreamNonBlocking));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_g, hipEventDisableTiming));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_r, hipEventDisableTiming));
-        // NNGP_BATCH_CU_RESERVE = R > 0: the overlapped batch's stream may not use R CUs (spread over
-        // the device), so the sweep's latency-bound launches (select, mean, G) always find a free CU
-        // instead of queueing behind the batch's long-lived work-queue workgroups (read once, when
-        // the stream is created)
-        const int reserve = env_int("NNGP_BATCH_CU_RESERVE", 0);
-        int ncu = 0;
-        NNGP_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-        if (reserve > 0 && reserve < ncu) {
-            std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-            for (int cu = 0; cu < ncu; cu++) mask[cu / 32] |= 1u << (cu % 32);
-            const int stride = ncu / reserve;
-            for (int k = 0; k < reserve; k++) mask[(k * stride) / 32] &= ~(1u << ((k * stride) % 32));
-            NNGP_HIP_CHECK(hipExtStreamCreateWithCUMask(&r.st3, (uint32_t)mask.size(), mask.data()));
-        } else {
-            NNGP_HIP_CHECK(hipStreamCreateWithFlags(&r.st3, hipStreamNonBlocking));
-        }
+        NNGP_HIP_CHECK(hipStreamCreateWithFlags(&r.st3, hipStreamNonBlocking));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_pre, hipEventDisableTiming));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_sel, hipEventDisableTiming));
         NNGP_HIP_CHECK(hipEventCreateWithFlags(&r.ev_b, hipEventDisableTiming));

@@ -761,6 +761,14 @@ static double potf2_gemv_row(double y, const double *a, const double *x, int n, 
     return y - t;
 }
 
+/* Roundoff-sensitivity experiment only (tests/golden/gen_oracle_loops.py *_sumorder): 1 switches
+ * the GP solves and the -LML's two sums to another, equally valid summation order (dot products
+ * accumulated with fma in the opposite direction and subtracted once; sequential instead of
+ * pairwise sums) -- the kind of last-ulp difference between the restatement and XLA/OpenBLAS.
+ * The default 0 is the oracle.                                                               */
+static int g_sum_order = 0;
+void orc_set_sum_order(int o) { g_sum_order = o; }
+
 /* Cholesky + solves for K = psy*exp(c*D2) + jit*I.  Returns 0 ok, 1 if potrf fails.
  * The factorisation follows OpenBLAS dpotf2_L (potf2_dot / potf2_gemv_row above); on the
  * reference's own LML fixtures (tests/golden/lml.npz) its pass/fail bit agrees on 99.8 % of the
@@ -793,13 +801,23 @@ static int gp_factor(int m, const double *D2, const double *y, double c, double 
     double z[64];
     for (int i = 0; i < m; i++) {
         double s = y[i];
-        for (int k = 0; k < i; k++) s = s - L[i * m + k] * z[k];
+        if (g_sum_order) {   /* experiment: BLAS-style dot first, reversed, then one subtraction */
+            double d = 0.0;
+            for (int k = i - 1; k >= 0; k--) d = fma(L[i * m + k], z[k], d);
+            s = s - d;
+        } else
+            for (int k = 0; k < i; k++) s = s - L[i * m + k] * z[k];
         const double q = s * rinv_d[i];
         z[i] = fma(fma(-q, L[i * m + i], s), rinv_d[i], q);
     }
     for (int i = m - 1; i >= 0; i--) {
         double s = z[i];
-        for (int k = m - 1; k > i; k--) s = s - L[k * m + i] * alpha[k];
+        if (g_sum_order) {
+            double d = 0.0;
+            for (int k = i + 1; k < m; k++) d = fma(L[k * m + i], alpha[k], d);
+            s = s - d;
+        } else
+            for (int k = m - 1; k > i; k--) s = s - L[k * m + i] * alpha[k];
         const double q = s * rinv_d[i];
         alpha[i] = fma(fma(-q, L[i * m + i], s), rinv_d[i], q);
     }
@@ -815,9 +833,17 @@ double orc_nlml(int m, const double *D2, const double *y, double sx, double sy, 
     const double psy = nn_pow10(sy);
     if (gp_factor(m, D2, y, c, psy, jit, L, alpha)) return INFINITY;
     for (int i = 0; i < m; i++) tmp[i] = y[i] * alpha[i];
-    const double ydot = butterfly_sum(tmp, m);
+    double ydot = butterfly_sum(tmp, m);
     for (int i = 0; i < m; i++) tmp[i] = nn_log(L[i * m + i]);
-    const double slog = butterfly_sum(tmp, m);
+    double slog = butterfly_sum(tmp, m);
+    if (g_sum_order) {   /* experiment: sequential sums */
+        ydot = 0.0;
+        slog = 0.0;
+        for (int i = 0; i < m; i++) {
+            ydot = fma(y[i], alpha[i], ydot);
+            slog += nn_log(L[i * m + i]);
+        }
+    }
     const double res = -(((-0.5 * ydot) - slog) - ((double)m / 2) * LOG_2PI);
     if (isnan(res)) return INFINITY;
     return res;
@@ -973,16 +999,9 @@ typedef struct {
     double jit;
 } nlml_ctx_t;
 
-/* Roundoff-sensitivity experiment only (tests/golden/gen_oracle_loops.py *_lmlscale): every
- * Nelder-Mead objective value is multiplied by this factor -- 1 + 2^-52 is a one-ulp relative
- * perturbation of the -LML, the size of the difference between two libms or BLAS orders.  The
- * default 1.0 leaves the oracle exact (x * 1.0 == x). */
-static double g_lml_scale = 1.0;
-void orc_set_lml_scale(double s) { g_lml_scale = s; }
-
 static double nlml_fn(const double *x, void *vctx) {
     const nlml_ctx_t *c = (const nlml_ctx_t *)vctx;
-    return orc_nlml(c->m, c->D2, c->y, x[0], x[1], c->jit) * g_lml_scale;
+    return orc_nlml(c->m, c->D2, c->y, x[0], x[1], c->jit);
 }
 
 /* one hyper-parameter fit: NNGP_p._get_opt_par / opt_theta (models.py:228-260)              */

@@ -76,7 +76,7 @@ def lib():
                                   _dp, _dp, i32]
         L.orc_d2.argtypes = [_dp, i32, i32, _dp]
         L.orc_max_threads.restype = ctypes.c_int
-        L.orc_set_lml_scale.argtypes = [dbl]
+        L.orc_set_sum_order.argtypes = [i32]
         for fn in ('nn_exp', 'nn_log', 'nn_pow10', 'nn_sin', 'nn_cos', 'nn_sin_pi'):
             getattr(L, fn).argtypes = [dbl]
             getattr(L, fn).restype = dbl

@@ -8,7 +8,7 @@ here; the oracle is pinned to it by tests/test_oracle_golden.py.
 
     python tests/golden/gen_oracle_loops.py burgers_pub_nngp_s45   # ~30 min on 8 cores
     python tests/golden/gen_oracle_loops.py fhn800_n512_nngp       # ~15 min
-    python tests/golden/gen_oracle_loops.py burgers_pub_nngp_s45_lmlscale   # K's roundoff sensitivity
+    python tests/golden/gen_oracle_loops.py burgers_pub_nngp_s45_sumorder   # K's roundoff sensitivity
     python tests/golden/gen_oracle_loops.py tomlab256_nngp         # TomLab N=256 to convergence
 """
 import hashlib
@@ -84,13 +84,13 @@ def tomlab256():
 
 
 def main(which):
-    if which.startswith('burgers_pub') and 'lmlscale' in which:
-        # roundoff sensitivity of K on the published schedule: the same run with every -LML the
-        # Nelder-Mead fits see scaled by (1 + 2^-52), i.e. one ulp (oracle orc_set_lml_scale)
-        O.lib().orc_set_lml_scale(1.0 + 2.0 ** -52)
+    if which.startswith('burgers_pub') and 'sumorder' in which:
+        # roundoff sensitivity of K on the published schedule: the same run with the GP solves and
+        # -LML sums in another summation order (oracle orc_set_sum_order; not a parity fixture)
+        O.lib().orc_set_sum_order(1)
         o, sec = burgers_pub('nngp', 45)
         np.savez_compressed(os.path.join(HERE, f'{which}.npz'), k=o['k'], conv_int=np.array(o['conv_int']),
-                            converged=o['converged'], digest=u_digest(o['u']), seconds=sec, lml_scale=1.0 + 2.0 ** -52)
+                            converged=o['converged'], digest=u_digest(o['u']), seconds=sec, sum_order=1)
     elif which.startswith('burgers_pub'):
         model = 'parareal' if 'para' in which.split('_')[2] else 'nngp'
         seed = int(which.rsplit('_s', 1)[1]) if model == 'nngp' else 0
