@@ -31,11 +31,11 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector: half the 157.3 TF FP32 vector pe
 HBM_PEAK_GBS = 8000.0
 # One-wave issue floor of the fine-sweep kernel: a slice is one dependent chain, so
 # a step costs (VALU per step) x (cycles per wave64 VALU issue).  The Hopf sweep at 128 slices runs
-# the lane-group kernel (components across a 16-lane group): 97 VALU per RK4 step in the gfx950
-# code object (tools/isa_loop_count.py rk_group_kernelILi1ELi4ELb0ELb1E; the one-lane-per-slice
-# kernel has 119); 4.22 cycles per independent v_mul/v_add_f64 and a 2.40 GHz shader clock
-# measured on the box (tools/ubench_fp64.hip).
-LANE_VALU_PER_STEP = 97
+# the lane-group kernel (components across a 16-lane group): 85 VALU per RK4 step in the gfx950
+# code object since round 3's carried bank-masked RHS registers (97 before; tools/isa_loop_count.py
+# rk_group_kernelILi1ELi4ELb0ELb1E; the one-lane-per-slice kernel has 119); 4.22 cycles per
+# independent v_mul/v_add_f64 and a 2.40 GHz shader clock measured on the box (tools/ubench_fp64.hip).
+LANE_VALU_PER_STEP = 85
 CYCLES_PER_F64_VALU = 4.22
 SHADER_GHZ = 2.40
 # algorithmic flops per fine step per slice: S*F_rhs + (2 nnz(a) + S + 2 nnz(b))*d

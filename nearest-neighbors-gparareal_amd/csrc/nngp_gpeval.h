@@ -161,7 +161,7 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
         for (int q = 0; q < NQ; q++) {
             if (q < P.nq) {
                 const int ix = P.idxq[q];
-                double e = psy * nn_exp(c * sD2[(ix >> 16) & 0x3FF]);    // k_gauss, models.py:146-148
+                double e = psy * nn_exp_nonpos(c * sD2[(ix >> 16) & 0x3FF]);   // k_gauss, models.py:146-148
                 if (ix >> 30) e = e + jit;                                // + eye*10**jitter, :88
                 Kimg[ix & 0xFFFF] = e;
             }
@@ -187,7 +187,7 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
                 if (j >= 16 * (s + 1)) continue;
                 double e = (row >= m && j == row) ? 1.0 : 0.0;
                 if (row < m && j <= row) {
-                    e = psy * nn_exp(c * sD2[row * m + j]);
+                    e = psy * nn_exp_nonpos(c * sD2[row * m + j]);
                     if (j == row) e = e + jit;
                 }
                 a[s][j] = e;
@@ -217,6 +217,16 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
     // kernel is singular for their jitter -- near-duplicate neighbours, FHN-PDE at its steady
     // state -- evaluate +inf until maxfev (~8 % of a d = 800 correction's fits, the whole tail).
     bool dead = false;   // wave-uniform
+    // The pivot's ddot, carried: ddot's accumulators over whole 4-column blocks depend only on the
+    // block, so each lane adds every finished block of its OWN rows (D1, D2 per row set) once, as
+    // the block's last column completes; column j then needs only D*[SJ] and its 0-3 tail
+    // columns (same sums, same order: one block's terms per step instead of all of row j's).
+    double D1[RPL], D2[RPL];
+#pragma unroll
+    for (int s = 0; s < RPL; s++) {
+        D1[s] = 0.0;
+        D2[s] = 0.0;
+    }
     static_for<0, MAXM>([&](auto jc) {
         constexpr int j = decltype(jc)::value, SJ = j / 16, LJ = j % 16;
         if (dead) return;
@@ -229,7 +239,6 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
                 tt[s] = 0.0;
                 blk[s] = 0.0;
             }
-        double d1 = 0.0, d2 = 0.0;   // the pivot row's ddot (row j lives in set SJ, lane LJ)
 #pragma unroll
         for (int k = 0; k < j; k++) {
             const double ljk = row_bcast<LJ>(a[SJ][k]);
@@ -245,15 +254,12 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
                     }
                     tt[s] = fma(ak, ljk, tt[s]);
                 }
-            // pivot ddot over the row-j owner's own entries L_jk (its set SJ)
-            const double xk = a[SJ][k];
-            if (k < (j & ~3)) {
-                if (k % 4 == 2) d1 = d1 + fma(a[SJ][k - 2], a[SJ][k - 2], xk * xk);
-                if (k % 4 == 3) d2 = d2 + fma(a[SJ][k - 2], a[SJ][k - 2], xk * xk);
-            } else {
-                d1 = fma(xk, xk, d1);
-            }
         }
+        // pivot ddot of the row-j owner's own entries L_jk (its set SJ): the carried blocks, then
+        // the tail columns (j & ~3) .. j-1
+        double d1 = D1[SJ], d2 = D2[SJ];
+#pragma unroll
+        for (int k = j & ~3; k < j; k++) d1 = fma(a[SJ][k], a[SJ][k], d1);
         // Pins (two row sets per lane): an empty asm that takes and returns each column's sums,
         // then each finished column.  Nothing is recomputed or reordered arithmetically -- the
         // asm is the identity on the bits -- but LLVM may no longer sink a row set's updates
@@ -270,21 +276,41 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
 #pragma unroll
         for (int s = 0; s < RPL; s++)
             if (16 * (s + 1) > j) t[s] = (l + 16 * s >= tail_start) ? a[s][j] - tt[s] : yv[s];
-        t[SJ] = (l == LJ) ? a[SJ][j] - (d1 + d2) : t[SJ];
-        const double piv = row_bcast<LJ>(t[SJ]);
+        // every lane forms the ddot pivot of its own set-SJ row; lane LJ's is row j's
+        const double piv = row_bcast<LJ>(a[SJ][j] - (d1 + d2));
         fail = fail || !(piv > 0.0);
         dead = __all(fail);
-        const double ljj = sqrt(piv);
-        const double ri = 1.0 / ljj;
+        // the pivot's sqrt and reciprocal: the short sequences when every live row's pivot is in
+        // their range (always, in practice), the full ones otherwise -- the same bits either way
+        double ljj, ri;
+        if (__all(fail || in_mid_range(piv))) {
+            ljj = sqrt_mid(piv);
+            ri = rcp_mid(ljj);
+        } else {
+            ljj = sqrt(piv);
+            ri = 1.0 / ljj;
+        }
         diag[SJ] = (l == LJ) ? ljj : diag[SJ];
         rinv[SJ] = (l == LJ) ? ri : rinv[SJ];
+        // (the owner's diagonal entry a[SJ][j] becomes t*ri too: nothing reads it -- the solves
+        // take L_jj from diag[], and the row-j updates they make after capturing z_j / alpha_j are
+        // the harmless ones noted there)
 #pragma unroll
         for (int s = 0; s < RPL; s++)
-            if (16 * (s + 1) > j) a[s][j] = (l + 16 * s == j) ? ljj : t[s] * ri;
+            if (16 * (s + 1) > j) a[s][j] = t[s] * ri;
         if constexpr (GP<MAXM>::PIN) {
 #pragma unroll
             for (int s = 0; s < RPL; s++)
                 if (16 * (s + 1) > j) asm volatile("" : "+v"(a[s][j]));
+        }
+        // a finished 4-column block: fold it into the carried ddot of every set with rows past j
+        if constexpr (j % 4 == 3) {
+#pragma unroll
+            for (int s = 0; s < RPL; s++)
+                if (16 * (s + 1) - 1 > j) {
+                    D1[s] = D1[s] + fma(a[s][j - 3], a[s][j - 3], a[s][j - 1] * a[s][j - 1]);
+                    D2[s] = D2[s] + fma(a[s][j - 2], a[s][j - 2], a[s][j] * a[s][j]);
+                }
         }
     });
     if (dead) {
@@ -394,7 +420,7 @@ __device__ __forceinline__ double gp_mean(int m, int l, const GPLane<MAXM> &P, c
 #pragma unroll
     for (int s = 0; s < RPL; s++) {
         const int row = l + 16 * s;
-        ka[s] = (psy * nn_exp(c * skd2[row < m ? row : 0])) * alpha[s];
+        ka[s] = (psy * nn_exp_nonpos(c * skd2[row < m ? row : 0])) * alpha[s];
     }
     const double mean = gp_rows_sum<RPL>(m, l, ka);
     return ok ? mean : NAN;

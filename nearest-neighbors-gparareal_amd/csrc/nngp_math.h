@@ -27,12 +27,17 @@ struct MathC {
 
 // exp(hi + lo) with |lo| << |hi|.  Branch-free (selects) so it inlines cheaply inside the
 // unrolled kernel-row loops; identical results to the oracle's branchy form.
-__device__ __forceinline__ double nn_exp_dd(double hi, double lo) {
-    const double xc = fmin(fmax(hi, -746.0), 710.0);   // keeps n in int range; NaN -> -746
+// NONPOS: hi <= 0 or NaN, lo == 0 (the SE kernel's c*D2 with c < 0 <= D2, models.py:146-148) --
+// the same bits with three ops fewer: the upper clamp and the overflow select are never taken
+// there, and r + 0 only normalises the sign of a zero r, which no term of the polynomial sees
+// (p = fma(p, +-0, c) = c).
+template <bool NONPOS = false>
+__device__ __forceinline__ double nn_exp_t(double hi, double lo) {
+    const double xc = NONPOS ? fmax(hi, -746.0) : fmin(fmax(hi, -746.0), 710.0);   // NaN -> -746
     const double n = rint(xc * MathC::INV_LN2);
     double r = fma(-n, MathC::LN2_HI, xc);
     r = fma(-n, MathC::LN2_LO, r);
-    r = r + lo;
+    if constexpr (!NONPOS) r = r + lo;
     // sum_{j=0}^{13} r^j / j!
     double p = 1.0 / 6227020800.0;             // 1/13!
     p = fma(p, r, 1.0 / 479001600.0);          // 1/12!
@@ -49,12 +54,44 @@ __device__ __forceinline__ double nn_exp_dd(double hi, double lo) {
     p = fma(p, r, 1.0);
     p = fma(p, r, 1.0);
     double res = ldexp(p, (int)n);
-    res = (hi > MathC::EXP_OVF) ? __builtin_huge_val() : res;
+    if constexpr (!NONPOS) res = (hi > MathC::EXP_OVF) ? __builtin_huge_val() : res;
     res = (hi < MathC::EXP_UNF) ? 0.0 : res;
     return (hi != hi) ? hi : res;
 }
 
-__device__ __forceinline__ double nn_exp(double x) { return nn_exp_dd(x, 0.0); }
+__device__ __forceinline__ double nn_exp_dd(double hi, double lo) { return nn_exp_t<false>(hi, lo); }
+__device__ __forceinline__ double nn_exp(double x) { return nn_exp_t<false>(x, 0.0); }
+// exp(x) for x <= 0 or NaN only (see NONPOS)
+__device__ __forceinline__ double nn_exp_nonpos(double x) { return nn_exp_t<true>(x, 0.0); }
+
+// sqrt(x) and 1.0/x, correctly rounded, for x in [2^-500, 2^500]: the instruction sequences the
+// compiler emits for sqrt() and 1.0/x on gfx950 (rsq + Goldschmidt with two corrections; rcp +
+// two Newton steps + the Markstein quotient correction) without the range scaling (ldexp /
+// v_div_scale) and special-value fixups (v_cmp_class / v_div_fixup), which are identities on that
+// range -- the same bits, ~12 ops fewer per pair.  Callers check the range (wave-uniformly) and
+// keep sqrt() / 1.0/x for everything else.
+__device__ __forceinline__ double sqrt_mid(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    return fma(d, h, g);
+}
+__device__ __forceinline__ double rcp_mid(double b) {
+    double y = __builtin_amdgcn_rcp(b);
+    y = fma(y, fma(-b, y, 1.0), y);
+    y = fma(y, fma(-b, y, 1.0), y);
+    return fma(fma(-b, y, 1.0), y, y);   // q = 1*y; r = 1 - b q; q + r y
+}
+// x in [2^-500, 2^500] (NaN and negatives excluded): one compare on the high word
+__device__ __forceinline__ bool in_mid_range(double x) {
+    const unsigned hi = (unsigned)(__double_as_longlong(x) >> 32);
+    return hi - 0x20B00000u <= 0x5F300000u - 0x20B00000u;
+}
 
 // 10^x = exp(x ln10), x ln10 as a double-double (models.py: 10**sigma)
 __device__ __forceinline__ double nn_pow10(double x) {

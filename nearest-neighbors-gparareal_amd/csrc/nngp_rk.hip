@@ -26,6 +26,7 @@
 // the contracted one exports nngp_rk_dispatch_contracted, which nngp_rk_batch calls.
 
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include "nngp_math.h"
@@ -111,16 +112,39 @@ template <> struct GroupSys<NNGP_SYS_LORENZ> {   // systems.py:232-238, as LaneS
 };
 template <> struct GroupSys<NNGP_SYS_HOPF> {     // systems.py:148-154, as LaneSys<HOPF>
     static constexpr int G = 16;
+    // g = (u2/mu - u0*u0) - u1*u1; component 0: -u1 + u0*g, component 1: u0 + u1*g, component 2: 1.
+    // Fewer ops than broadcasting u0, u1, u2 and squaring the broadcasts: every lane squares its
+    // own component (sq = x*x, the same rounded products), and bank-masked `take`s into registers
+    // carried from stage to stage move only what banks 0 and 1 need -- u2 (for u2/mu), u0^2, u1^2
+    // and the coupling term P (bank 0: u1, bank 1: u0) -- while bank 2's lanes keep what `init`
+    // put there: 0 in C, A2, B2, so g = +-0 and x*g = +-0 (u2 is always finite), and 1.0 in P.
+    // The sum p + x*g is one fma(S, P, x*g) with S = -1 in bank 0 and +1 elsewhere: S*P is exact,
+    // so the fma is the correctly rounded x*g -+ P, bitwise the reference's addition (signed zeros
+    // included: the fma's exact-sum rule is the addition's); bank 2: +-0 + 1 = 1.
+    // 13 VALU per RHS instead of 16.  (The contracted build keeps the broadcast form, whose
+    // p + x*g contracts to one fma there.)
+#ifdef NNGP_RK_FMA
     __device__ static double f(double x, int c, double one, const LaneArgs &a) {
         const double A = bcast<0>(x), B = bcast<1>(x), C = bcast<2>(x);
         const double g = (div_const(C, a.param[0], a.rparam0) - A * A) - B * B;
-        // component 0: -u1 + u0*g, component 1: u0 + u1*g (own component times g), component 2: 1.
-        // p by v_cndmask: a take<4, 0x1>(A, -x) would read -x right after the VALU writing it (DPP
-        // hazard wait states) and copy A into its destination first -- measured slower (0.215 vs
-        // 0.208 us/step); the constant `one` has neither cost.
         const double p = c == 0 ? -B : A;
         return take<8, 0x4>(p + x * g, one);
     }
+#else
+    struct St {
+        double C, A2, B2, P, S;
+    };
+    __device__ static St init(int c) { return St{0.0, 0.0, 0.0, c == 2 ? 1.0 : 0.0, c == 0 ? -1.0 : 1.0}; }
+    __device__ static double f(double x, St &s, double, const LaneArgs &a) {
+        const double sq = x * x;
+        s.C = take<8, 0x3>(s.C, x);
+        s.A2 = take<0, 0x3>(s.A2, sq);
+        s.B2 = take<4, 0x3>(s.B2, sq);
+        s.P = take<0, 0x2>(take<4, 0x1>(s.P, x), x);
+        const double g = (div_const(s.C, a.param[0], a.rparam0) - s.A2) - s.B2;
+        return __builtin_fma(s.S, s.P, x * g);
+    }
+#endif
 };
 template <> struct GroupSys<NNGP_SYS_THOMAS_LABYRINTH> {   // systems.py:257-271
     static constexpr int G = 4;
@@ -174,6 +198,17 @@ template <> struct GroupSys<NNGP_SYS_DBL_PEND> {  // systems.py:182-189, as Lane
     }
 };
 
+// Per-lane state a group RHS carries from stage to stage (GroupSys<SYS>::St, made by its init(c));
+// a field without one gets its component index.
+template <class GS, class = void> struct GroupState {
+    using T = int;
+    __device__ static int init(int c) { return c; }
+};
+template <class GS> struct GroupState<GS, std::void_t<typename GS::St>> {
+    using T = typename GS::St;
+    __device__ static T init(int c) { return GS::init(c); }
+};
+
 template <int SYS> struct has_group { static constexpr bool value = false; };
 template <> struct has_group<NNGP_SYS_LORENZ> { static constexpr bool value = true; };
 template <> struct has_group<NNGP_SYS_HOPF> { static constexpr bool value = true; };
@@ -201,6 +236,7 @@ __global__ void __launch_bounds__(64) rk_group_kernel(LaneArgs args, int n_slice
     const bool own = c < D;
     const bool writer = own && (G != 16 || (tid & 3) == 0);
     const double one = 1.0;
+    typename GroupState<GroupSys<SYS>>::T gst = GroupState<GroupSys<SYS>>::init(c);
     double mn = 0, hw = 0, sc = 0;
     if constexpr (NORM) {
         if (own) {
@@ -221,8 +257,8 @@ __global__ void __launch_bounds__(64) rk_group_kernel(LaneArgs args, int n_slice
         for (int s = 0; s < S; s++) {
             const double tmp = stage_input<T, 1>(s, u, k, 0);
             double o;
-            if constexpr (NORM) o = GroupSys<SYS>::f((tmp + 1) * hw + mn, c, one, args) * sc;
-            else o = GroupSys<SYS>::f(tmp, c, one, args);
+            if constexpr (NORM) o = GroupSys<SYS>::f((tmp + 1) * hw + mn, gst, one, args) * sc;
+            else o = GroupSys<SYS>::f(tmp, gst, one, args);
             k[s] = h * o;
         }
         u = step_update<T, 1>(u, k, 0);

@@ -3,7 +3,11 @@
 // of the evaluation core can be compared quickly.
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off -DUB_MAXM=20 \
 //        -Rpass-analysis=kernel-resource-usage tools/ubench_gpeval.hip -o tools/_ubench_gpeval
+#ifdef UB_HEADER   // another copy of the evaluation core, for old/new comparisons
+#include UB_HEADER
+#else
 #include "../nearest-neighbors-gparareal_amd/csrc/nngp_gpeval.h"
+#endif
 
 #include <cstdio>
 #include <cstring>
