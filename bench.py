@@ -240,7 +240,7 @@ def fhn_pde_converge(torch, g, dx=20, ng=50, nf=195325):
 
 
 def _maxm(m):
-    for M in (8, 16, 20, 24, 32, 48, 64):
+    for M in (8, 16, 18, 20, 24, 32, 48, 64):
         if m <= M:
             return M
     return m

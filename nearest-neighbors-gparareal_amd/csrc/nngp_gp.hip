@@ -1474,15 +1474,17 @@ static int fill_jitters(NMArgs &a, int n_jitter, const double *jexp) {
     return NNGP_OK;
 }
 
-// padded fit size: the kernel instantiations (8, 16, 20, 24, 32, 48, 64)
+// padded fit size: the kernel instantiations (8, 16, 18, 20, 24, 32, 48, 64).  18 is there so
+// that 20 serves m = 19, 20 only, whose row set 0 never holds a tail row (GP<MAXM>::tail_set)
 static constexpr int MAX_M = 64;
 static int maxm_for(int m) {
-    return m <= 8 ? 8 : (m <= 16 ? 16 : (m <= 20 ? 20 : (m <= 24 ? 24 : (m <= 32 ? 32 : (m <= 48 ? 48 : 64)))));
+    return m <= 8 ? 8 : (m <= 16 ? 16 : (m <= 18 ? 18 : (m <= 20 ? 20 : (m <= 24 ? 24 : (m <= 32 ? 32 : (m <= 48 ? 48 : 64))))));
 }
 static size_t k_image_doubles(int maxm) {
     switch (maxm) {
     case 8: return GP<8>::IMG;
     case 16: return GP<16>::IMG;
+    case 18: return GP<18>::IMG;
     case 20: return GP<20>::IMG;
     case 24: return GP<24>::IMG;
     case 32: return GP<32>::IMG;
@@ -1501,6 +1503,7 @@ static int with_maxm(int m, F &&f) {
     switch (maxm_for(m)) {
     case 8: return f(std::integral_constant<int, 8>{});
     case 16: return f(std::integral_constant<int, 16>{});
+    case 18: return f(std::integral_constant<int, 18>{});
     case 20: return f(std::integral_constant<int, 20>{});
     case 24: return f(std::integral_constant<int, 24>{});
     case 32: return f(std::integral_constant<int, 32>{});
@@ -2025,6 +2028,7 @@ int chain_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t 
     switch (maxm) {
     case 8: rc = chain_launch<8>(c, nb, lds, st); break;
     case 16: rc = chain_launch<16>(c, nb, lds, st); break;
+    case 18: rc = chain_launch<18>(c, nb, lds, st); break;
     case 20: rc = chain_launch<20>(c, nb, lds, st); break;
     case 24: rc = chain_launch<24>(c, nb, lds, st); break;
     default: rc = chain_launch<32>(c, nb, lds, st); break;

@@ -69,7 +69,7 @@ __device__ __forceinline__ void static_for(F &&f) {
     }
 }
 
-// A fit of size m runs padded to MAXM (one of 8, 16, 20, 24, 32, 48, 64): rows m..MAXM-1 are
+// A fit of size m runs padded to MAXM (one of 8, 16, 18, 20, 24, 32, 48, 64): rows m..MAXM-1 are
 // identity rows of K with y = 0.  The padded factorisation is exact -- L = [[L_m, 0], [0, I]], z
 // and alpha pad with exact zeros, every real row's arithmetic is untouched -- so every loop has a
 // compile-time trip count and no per-j branches.
@@ -79,8 +79,15 @@ __device__ __forceinline__ void static_for(F &&f) {
 // lane, each lane builds its own rows' exps in registers (no redistribution), and the LDS image
 // is the PACKED lower triangle (row r at r(r+1)/2) that only the back solve reads -- a full image
 // would not fit four fits per workgroup in LDS at m = 64.
+// the padded sizes, and the smallest m each one serves
+__host__ __device__ constexpr int gp_mmin(int maxm) {
+    return maxm <= 8 ? 1 : maxm <= 16 ? 9 : maxm <= 18 ? 17 : maxm <= 20 ? 19 : maxm <= 24 ? 21
+         : maxm <= 32 ? 25 : maxm <= 48 ? 33 : 49;
+}
+
 template <int MAXM_> struct GP {
     static constexpr int MAXM = MAXM_;
+    static constexpr int MMIN = gp_mmin(MAXM_);
     static constexpr int RPL = (MAXM + 15) / 16;                        // rows per lane
     static constexpr bool BIG = MAXM > 32;
     static constexpr int S = MAXM + 1;                                  // LDS row stride (pad)
@@ -89,6 +96,11 @@ template <int MAXM_> struct GP {
     // two row sets per lane (MAXM 20..32): the column pins of gp_factor (see there)
     static constexpr bool PIN = RPL == 2 && !BIG;
     static constexpr int NQ = BIG ? 1 : (MAXM * (MAXM + 1) / 2 + 15) / 16;   // triangle entries / lane
+    // can row set s hold a "tail row" of dpotf2's column update (the last (m-1-j) & 3 rows under
+    // column j, all >= m - 3 >= MMIN - 3)?  If not, its rows always take the vector-row form and
+    // the tail form's fma chain and select are not evaluated: for MAXM = 20 (m = 19, 20) set 0
+    // skips 120 fma and 16 selects per evaluation.
+    static constexpr bool tail_set(int s) { return 16 * s + 15 >= MMIN - 3; }
 };
 // LDS offset of K/L entry (r, j), j <= r, in a fit's image
 template <int MAXM>
@@ -198,7 +210,17 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
     //    broadcast, so every lane computes L_jj and RN(1/L_jj) identically; the row owner keeps
     //    them.  Updates of rows < j (upper triangle) are computed and ignored: fewer
     //    instructions than masking them.
-    bool fail = false;
+    // The lane index, opaque to LLVM: every per-column lane mask ((lane == j % 16), row >=
+    // tail_start) is then one v_cmp where it is used.  Visible, LLVM hoisted all of them out of
+    // the Nelder-Mead loop as 64-bit SGPR masks, ran out of SGPRs and spilled them to VGPR lanes:
+    // two v_readlane per use instead of one compare (and VGPRs held for the spill slots).
+    // m likewise (wave-uniform, an SGPR): the per-column tail_start is then two SALU ops where
+    // it is used instead of a spilled constant read back by v_readlane.
+    int lo = l, mo = m;
+    asm volatile("" : "+v"(lo), "+s"(mo));
+    // failed pivots as a wave mask (SGPRs): a per-lane bool OR-ed across columns is rebuilt into
+    // a mask by a v_cndmask / v_cmp pair at every __all
+    uint64_t fmask = 0;
     double rinv[RPL];
 #pragma unroll
     for (int s = 0; s < RPL; s++) {
@@ -230,7 +252,7 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
     static_for<0, MAXM>([&](auto jc) {
         constexpr int j = decltype(jc)::value, SJ = j / 16, LJ = j % 16;
         if (dead) return;
-        const int tail_start = j + 1 + ((m - 1 - j) & ~3);
+        const int tail_start = j + 1 + ((mo - 1 - j) & ~3);
         double yv[RPL], tt[RPL], blk[RPL];
 #pragma unroll
         for (int s = 0; s < RPL; s++)
@@ -252,7 +274,7 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
                     } else {
                         yv[s] = yv[s] - ak * ljk;
                     }
-                    tt[s] = fma(ak, ljk, tt[s]);
+                    if (GP<MAXM>::tail_set(s)) tt[s] = fma(ak, ljk, tt[s]);
                 }
         }
         // pivot ddot of the row-j owner's own entries L_jk (its set SJ): the carried blocks, then
@@ -269,29 +291,33 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
         if constexpr (GP<MAXM>::PIN) {
 #pragma unroll
             for (int s = 0; s < RPL; s++)
-                if (16 * (s + 1) > j) asm volatile("" : "+v"(yv[s]), "+v"(tt[s]));
-            asm volatile("" : "+v"(d1), "+v"(d2));
+                if (16 * (s + 1) > j) {
+                    if (GP<MAXM>::tail_set(s)) asm volatile("" : "+v"(yv[s]), "+v"(tt[s]));
+                    else asm volatile("" : "+v"(yv[s]));
+                }
         }
         double t[RPL];
 #pragma unroll
         for (int s = 0; s < RPL; s++)
-            if (16 * (s + 1) > j) t[s] = (l + 16 * s >= tail_start) ? a[s][j] - tt[s] : yv[s];
+            if (16 * (s + 1) > j)
+                t[s] = (GP<MAXM>::tail_set(s) && lo + 16 * s >= tail_start) ? a[s][j] - tt[s] : yv[s];
         // every lane forms the ddot pivot of its own set-SJ row; lane LJ's is row j's
         const double piv = row_bcast<LJ>(a[SJ][j] - (d1 + d2));
-        fail = fail || !(piv > 0.0);
-        dead = __all(fail);
+        fmask |= __builtin_amdgcn_ballot_w64(!(piv > 0.0));
+        const uint64_t live = __builtin_amdgcn_read_exec();
+        dead = fmask == live;
         // the pivot's sqrt and reciprocal: the short sequences when every live row's pivot is in
         // their range (always, in practice), the full ones otherwise -- the same bits either way
         double ljj, ri;
-        if (__all(fail || in_mid_range(piv))) {
+        if ((fmask | __builtin_amdgcn_ballot_w64(in_mid_range(piv))) == live) {
             ljj = sqrt_mid(piv);
             ri = rcp_mid(ljj);
         } else {
             ljj = sqrt(piv);
             ri = 1.0 / ljj;
         }
-        diag[SJ] = (l == LJ) ? ljj : diag[SJ];
-        rinv[SJ] = (l == LJ) ? ri : rinv[SJ];
+        diag[SJ] = (lo == LJ) ? ljj : diag[SJ];
+        rinv[SJ] = (lo == LJ) ? ri : rinv[SJ];
         // (the owner's diagonal entry a[SJ][j] becomes t*ri too: nothing reads it -- the solves
         // take L_jj from diag[], and the row-j updates they make after capturing z_j / alpha_j are
         // the harmless ones noted there)
@@ -334,7 +360,7 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
     static_for<0, MAXM>([&](auto ic) {
         constexpr int i = decltype(ic)::value, SI = i / 16, LI = i % 16;
         const double zi = row_bcast<LI>(divd(SI, acc[SI]));
-        z[SI] = (l == LI) ? zi : z[SI];
+        z[SI] = (lo == LI) ? zi : z[SI];
 #pragma unroll
         for (int s = 0; s < RPL; s++)
             if (16 * (s + 1) > i + 1) acc[s] = acc[s] - a[s][i] * zi;
@@ -366,13 +392,13 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
     static_for<0, MAXM>([&](auto ic) {
         constexpr int i = MAXM - 1 - decltype(ic)::value, SI = i / 16, LI = i % 16;
         const double ai = row_bcast<LI>(divd(SI, acc2[SI]));
-        alpha[SI] = (l == LI) ? ai : alpha[SI];
+        alpha[SI] = (lo == LI) ? ai : alpha[SI];
 #pragma unroll
         for (int s = 0; s < RPL; s++)
             if (16 * s < i)   // L[i][row]; rows past MAXM (pads, never read) clamp to the image
                 acc2[s] = acc2[s] - Kimg[img_at<MAXM>(i, min(l + 16 * s, MAXM - 1))] * ai;
     });
-    return !fail;
+    return !((fmask >> (__lane_id() & 63)) & 1);
 }
 
 // sum over the fit's rows r < m of v[r]: each lane adds its rows l, l+16, l+32, ... left to right

@@ -422,7 +422,39 @@ __global__ void __launch_bounds__(EPT == 1 ? 1024 : (EPT == 2 ? 512 : 256)) rk_f
 // Laplacians (the own and partner values come from registers): 1 write + 10 reads per point
 // instead of the element-per-thread kernel's 2 writes + 14 reads.  Same expressions, same order
 // (systems.py:365-366) -- bitwise rk_field_kernel<FHN_PDE>.  d = 2 nx^2 <= 2048.
+//
+// LDS layout: FHN_PAIR_IMAGES images of [u | v], each field at a fixed stride of FHN_PAIR_PS
+// doubles, and a stage's image fixed at compile time (stage s of every step uses image s & 1, the
+// last of an odd stage count image 2, so the image a stage writes was last read two barriers
+// earlier).  Every LDS access of the step loop is then one of five per-thread neighbour addresses
+// plus an immediate offset: no address arithmetic per stage (round 2 recomputed buf * d + c_i
+// for all ten reads and two writes of every stage, ~11 of its ~70 VALU).  Threads past the grid
+// (the last wave's idle lanes) compute point 0's stencil on their own zeros and write their
+// garbage to the images' padding, so the step loop has no branch either.
 // ---------------------------------------------------------------------------------------------
+// doubles per field image (half <= 1024).  At 1024 the u and v reads of a neighbour merge into one
+// ds_read2st64_b64 (and the two writes into one ds_write2st64_b64); measured the same as 1025 (ten
+// separate ds_read_b64): d = 800, 512 slices 6.34 / 6.35 us per RK8 step, 64 slices 3.66 / 3.67
+// (profiles/r03/field_probe_h.txt)
+static constexpr int FHN_PAIR_PS = 1024;
+
+template <int S> struct FhnPairImages {
+    static constexpr int N = (S % 2 == 1 && S > 1) ? 3 : 2;
+    // image of stage s (S == 1 alternates at run time)
+    static constexpr int of(int s) { return (S % 2 == 1 && s == S - 1) ? 2 : (s & 1); }
+};
+
+// ((a L)@v)_p as fhn_lap, the five coefficients selected once per thread
+__device__ __forceinline__ double fhn_lap5(const double *__restrict__ V, const Nbr5 &nb, double k0, double k1,
+                                           double k2, double k3, double k4) {
+    double s = k0 * V[nb.c0];
+    s = s + k1 * V[nb.c1];
+    s = s + k2 * V[nb.c2];
+    s = s + k3 * V[nb.c3];
+    s = s + k4 * V[nb.c4];
+    return s;
+}
+
 template <int ORDER, bool LINSPACE, bool NORM>
 __global__ void __launch_bounds__(1024) rk_fhn_pair_kernel(FieldArgs fa, int n_slices,
                                                            const double *__restrict__ t0,
@@ -431,8 +463,9 @@ __global__ void __launch_bounds__(1024) rk_fhn_pair_kernel(FieldArgs fa, int n_s
                                                            const double *__restrict__ u0,
                                                            double *__restrict__ uF) {
     using T = Tableau<ORDER>;
-    constexpr int S = T::S;
-    extern __shared__ __attribute__((aligned(16))) double smem[];   // [2][d]
+    using IM = FhnPairImages<T::S>;
+    constexpr int S = T::S, PS = FHN_PAIR_PS;
+    extern __shared__ __attribute__((aligned(16))) double smem[];   // [IM::N][2][PS]
     const int slice = blockIdx.x;
     const int p = threadIdx.x;
     const int d = fa.d, half = d / 2;
@@ -451,40 +484,43 @@ __global__ void __launch_bounds__(1024) rk_fhn_pair_kernel(FieldArgs fa, int n_s
         }
     }
     const Nbr5 nb = fhn_neighbours(fa.nx, ok ? p : 0);   // the same stencil for u and v
+    const double ka0 = nb.d0 ? fa.a_diag : fa.a_off, ka1 = nb.d1 ? fa.a_diag : fa.a_off,
+                 ka2 = nb.d2 ? fa.a_diag : fa.a_off, ka3 = nb.d3 ? fa.a_diag : fa.a_off,
+                 ka4 = nb.d4 ? fa.a_diag : fa.a_off;
+    const double kb0 = nb.d0 ? fa.b_diag : fa.b_off, kb1 = nb.d1 ? fa.b_diag : fa.b_off,
+                 kb2 = nb.d2 ? fa.b_diag : fa.b_off, kb3 = nb.d3 ? fa.b_diag : fa.b_off,
+                 kb4 = nb.d4 ? fa.b_diag : fa.b_off;
     const double T0 = t0[slice], T1 = t1[slice];
     const double dt = (T1 - T0) / (double)(LINSPACE ? gsteps : steps);
     const int64_t j0 = j0s ? j0s[slice] : 0;
-    int buf = 0;
     LinGrid grid;
     if constexpr (LINSPACE) grid.init(j0, gsteps, T0, dt);
     for (int64_t n = 0; n < steps; n++) {
         const double h = LINSPACE ? grid.next(n, T0, T1, dt) : dt;
 #pragma unroll
         for (int s = 0; s < S; s++) {
-            double *V = smem + buf * d;
+            const int img = (S == 1) ? (int)(n & 1) : IM::of(s);
+            double *V = smem + img * 2 * PS;
             double xw[2];
 #pragma unroll
             for (int r = 0; r < 2; r++) {
                 const double x = stage_input<T, 2>(s, u[r], k, r);
                 xw[r] = NORM ? (x + 1) * w[r] + mn[r] : x;
-                if (ok) V[p + r * half] = xw[r];
+                V[p + r * PS] = xw[r];
             }
             __syncthreads();
-            double fu = 0.0, fv = 0.0;
-            if (ok) {   // systems.py:365-366, as rk_field_kernel with V[e] / V[half+e] / V[e-half] in registers
-                const double lu = fhn_lap(V, nb, fa.a_off, fa.a_diag);
-                const double u1 = xw[0], u1c = u1 * (u1 * u1);
-                fu = (((lu + u1) - u1c) - xw[1]) + -5E-3 * 1.0;
-                const double lv = fhn_lap(V + half, nb, fa.b_off, fa.b_diag);
-                fv = (1 / 0.1) * ((lv + xw[0]) - xw[1]);
-                if (NORM) {
-                    fu = fu * sc[0];
-                    fv = fv * sc[1];
-                }
+            // systems.py:365-366, as rk_field_kernel with V[e] / V[half+e] / V[e-half] in registers
+            const double lu = fhn_lap5(V, nb, ka0, ka1, ka2, ka3, ka4);
+            const double u1 = xw[0], u1c = u1 * (u1 * u1);
+            double fu = (((lu + u1) - u1c) - xw[1]) + -5E-3 * 1.0;
+            const double lv = fhn_lap5(V + PS, nb, kb0, kb1, kb2, kb3, kb4);
+            double fv = (1 / 0.1) * ((lv + xw[0]) - xw[1]);
+            if (NORM) {
+                fu = fu * sc[0];
+                fv = fv * sc[1];
             }
             k[s * 2 + 0] = h * fu;
             k[s * 2 + 1] = h * fv;
-            buf ^= 1;
         }
 #pragma unroll
         for (int r = 0; r < 2; r++) u[r] = step_update<T, 2>(u[r], k, r);   // RK.py:170
@@ -726,7 +762,7 @@ static int launch_field(const nngp_system *sys, int n, const double *t0, const d
         const char *pe = getenv("NNGP_FHN_PAIR");
         if (!pe || atoi(pe) != 0) {
             const int bt = ((sys->d / 2 + 63) / 64) * 64;
-            const size_t lds = sizeof(double) * 2 * (size_t)sys->d;
+            const size_t lds = sizeof(double) * 2 * FHN_PAIR_PS * FhnPairImages<Tableau<ORDER>::S>::N;
             if (fa.normalized)
                 hipLaunchKernelGGL((rk_fhn_pair_kernel<ORDER, LIN, true>), dim3(n), dim3(bt), lds, st, fa, n, t0, t1,
                                    steps, gsteps, j0, u0, uF);

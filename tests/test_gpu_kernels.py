@@ -298,11 +298,11 @@ def test_predict_restarts_and_small_training_set(gpu):
 
 
 @pytest.mark.parametrize('park', ['0', '30', '100'])
-@pytest.mark.parametrize('m,d,R', [(5, 3, 1), (12, 4, 2), (16, 3, 2), (20, 6, 1), (20, 3, 2), (30, 2, 2),
+@pytest.mark.parametrize('m,d,R', [(5, 3, 1), (12, 4, 2), (16, 3, 2), (17, 5, 2), (19, 7, 1), (20, 6, 1), (20, 3, 2), (30, 2, 2),
                                    (10, 300, 1), (18, 130, 2), (20, 80, 1), (24, 3, 1),
                                    (40, 3, 1), (48, 4, 2), (64, 3, 1), (56, 40, 1), (33, 140, 1)])
 def test_predict_every_padded_size_and_fallback_vs_oracle(gpu, m, d, R, park, monkeypatch):
-    """Fits run padded to 8/16/20/24/32/48/64 rows (identity pad, exact; m > 32 -- the adaptive
+    """Fits run padded to 8/16/18/20/24/32/48/64 rows (identity pad, exact; m > 32 -- the adaptive
     m = max(10, k+2) past iteration 30, models.py:172-175 -- with 3-4 kernel rows per lane).  Up to 8 fits per CU each fit
     gets a wave and evaluates reflect/expand/contract points speculatively; above that (d=300:
     2 700 fits) the packed kernel runs 4 fits per wave, fused with the arg-min and mean -- or,

@@ -36,6 +36,7 @@ def test_lorenz_nngp_k_distribution_matches_reference(gpu):
     (the reference itself moves 18 -> 17/19 under a 1-ulp perturbation), so K is
     compared as a distribution over the reference's seeds 45-49."""
     P = golden('para_lorenz.npz')
+    s = O.System('lorenz')
     ks, ref = [], []
     for seed in (45, 46, 47, 48, 49):
         r = _lorenz(gpu).run(model='nngp', nn=10, seed=seed)
@@ -44,9 +45,15 @@ def test_lorenz_nngp_k_distribution_matches_reference(gpu):
         ref.append(int(P[f'nngp_s{seed}__k']))
         # converged solution vs the serial fine solution at the slice boundaries
         assert np.max(np.abs(r['u'][:, :, -1] - P['fine'])) < 0.1   # chaos amplifies eps = 5e-7
-    print('K gpu', ks, 'reference', ref)
-    assert max(abs(a - b) for a, b in zip(ks, ref)) <= 4
-    assert abs(np.mean(ks) - np.mean(ref)) <= 2
+        # every seed is the oracle's loop bit for bit (K, conv_int, iterates); the spread against
+        # the reference below is the restatement's fixed summation order, not the kernels
+        o = O.parareal(s, [0, 18], 32, 6, 450, 'RK4', 'RK4', model='nngp', nn=10, seed=seed,
+                       u0=s.fit([-15, -15, 20]))
+        assert r['k'] == o['k'] and r['conv_int'] == o['conv_int']
+        assert np.array_equal(np.nan_to_num(r['u'], nan=7.0), np.nan_to_num(o['u'], nan=7.0))
+    print('K gpu', ks, 'reference', ref)   # oracle = gpu: [18, 19, 18, 18, 18]; reference [18, 21, 18, 19, 20]
+    assert max(abs(a - b) for a, b in zip(ks, ref)) <= 2   # K within +-2 of the reference
+    assert abs(np.mean(ks) - np.mean(ref)) <= 1.5
     assert all(k < 32 for k in ks)   # nnGParareal beats plain Parareal (K=21) on average
     assert np.mean(ks) <= 21
 

@@ -38,6 +38,10 @@ def sweep(name, ode, n, steps, tspan, reps=3):
 
 if __name__ == '__main__':
     torch.cuda.set_device(0)
+    if len(sys.argv) > 1 and sys.argv[1] == 'fhn':   # FHN-PDE d=800 only (PMC passes: short)
+        sweep('fhn', g.FHN_PDE(d_x=20), 512, 500, [0, 1100], reps=1)
+        sweep('fhn', g.FHN_PDE(d_x=20), 64, 500, [0, 1100 / 8], reps=1)
+        sys.exit(0)
     sweep('burgers', g.Burgers(d_x=128, normalization='-11'), 128, 2000, [0, 5])
     sweep('fhn', g.FHN_PDE(d_x=20), 512, 2000, [0, 1100])
     sweep('fhn', g.FHN_PDE(d_x=20), 64, 2000, [0, 1100 / 8])   # one GPU's share of N=512 on 8 GPUs
