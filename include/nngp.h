@@ -196,7 +196,7 @@ int nngp_predict_range(const double *X, const double *Y, int64_t rows, int d, co
  *     fits; NNGP_SPEC_OVERLAP=0 serialises them); the call returns after both have drained.
  *   spec_hits_out: HOST, number of slices served by the speculative batch, or NULL;
  *   g_ms_out: HOST, total device time of the G launches (ms), or NULL (no timing events).
- * With NNGP_CHAIN=1, speculation on, an ODE or Burgers (d = 64k <= 256) system, exact G and m <= 32, the runs
+ * With NNGP_CHAIN=1, speculation on, an ODE or Burgers (d = 64k <= 256) system, exact G and m <= 24, the runs
  * of hit slices go through ONE persistent cooperative kernel (G, kNN, hit check, arg-min, mean
  * and update per slice, grid barriers between the phases; the host takes over at each miss):
  * bitwise the launch chain.  Opt-in (NNGP_CHAIN=1): measured not faster than the launch chain

@@ -1914,14 +1914,16 @@ static int chain_resources(ChainRes **out) {
 }
 
 // the systems / shapes the chain's in-kernel G covers (the rest keep the launch chain):
-// every ODE (lane form) and Burgers with d = 64*EPT <= 256 (wave form); exact G, m <= 32.
+// every ODE (lane form) and Burgers with d = 64*EPT <= 256 (wave form); exact G, m <= 24 (at the
+// padded size 32 the mean phase's 16 fit images -- K/L plus the per-row scalars -- and the select's
+// LDS no longer fit one CU's 160 KiB together).
 // Opt-in (NNGP_CHAIN=1): measured on the box it is bitwise the launch chain but not faster --
 // 0.90-1.00x on Lorenz / FHN-ODE / Hopf / Burgers (tools/chain_probe.py).
 bool chain_supported(const nngp_system *sys, int g_step_mode, int m) {
     const char *e = getenv("NNGP_CHAIN");
     if (!e || atoi(e) == 0) return false;
     if (g_step_mode & NNGP_STEP_CONTRACT) return false;
-    if (m < 1 || m > 32 || sys->d > CHAIN_QMAX) return false;
+    if (m < 1 || m > 24 || sys->d > CHAIN_QMAX) return false;
     switch (sys->kind) {
     case NNGP_SYS_LORENZ: case NNGP_SYS_HOPF: case NNGP_SYS_THOMAS_LABYRINTH: case NNGP_SYS_FHN_ODE:
     case NNGP_SYS_ROSSLER: case NNGP_SYS_BRUSSELATOR: case NNGP_SYS_DBL_PEND:

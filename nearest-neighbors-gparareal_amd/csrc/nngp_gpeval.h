@@ -91,8 +91,10 @@ template <int MAXM_> struct GP {
     static constexpr int RPL = (MAXM + 15) / 16;                        // rows per lane
     static constexpr bool BIG = MAXM > 32;
     static constexpr int S = MAXM + 1;                                  // LDS row stride (pad)
-    static constexpr int IMG = BIG ? 8 * RPL * (16 * RPL + 1)           // image doubles / fit
-                                   : MAXM * S;                          // (rows >= MAXM: no image)
+    static constexpr int XOFF = BIG ? 8 * RPL * (16 * RPL + 1)          // K/L image doubles / fit
+                                    : MAXM * S;                         // (rows >= MAXM: no image)
+    // then the fit's per-row scalars, L_jj | RN(1/L_jj) | z | alpha, MAXM each (gp_factor)
+    static constexpr int IMG = XOFF + 4 * MAXM;
     // two row sets per lane (MAXM 20..32): the column pins of gp_factor (see there)
     static constexpr bool PIN = RPL == 2 && !BIG;
     static constexpr int NQ = BIG ? 1 : (MAXM * (MAXM + 1) / 2 + 15) / 16;   // triangle entries / lane
@@ -207,9 +209,12 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
         }
     }
     // 3) left-looking Cholesky, row j broadcast from lane j%16 of set j/16.  The pivot is
-    //    broadcast, so every lane computes L_jj and RN(1/L_jj) identically; the row owner keeps
-    //    them.  Updates of rows < j (upper triangle) are computed and ignored: fewer
-    //    instructions than masking them.
+    //    broadcast, so every lane computes L_jj and RN(1/L_jj) identically, and every lane of the
+    //    row stores them to the fit's scalar slots Kx[j], Kx[MAXM + j] (the same value to the same
+    //    address from all 16 lanes: no lane mask, no VALU -- the owner-only select it replaces
+    //    was a v_cmp and two v_cndmask per value, or two v_readlane when LLVM spilled the masks;
+    //    z_i and alpha_i of the solves likewise).  Updates of rows < j (upper triangle) are
+    //    computed and ignored: fewer instructions than masking them.
     // The lane index, opaque to LLVM: every per-column lane mask ((lane == j % 16), row >=
     // tail_start) is then one v_cmp where it is used.  Visible, LLVM hoisted all of them out of
     // the Nelder-Mead loop as 64-bit SGPR masks, ran out of SGPRs and spilled them to VGPR lanes:
@@ -221,12 +226,13 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
     // failed pivots as a wave mask (SGPRs): a per-lane bool OR-ed across columns is rebuilt into
     // a mask by a v_cndmask / v_cmp pair at every __all
     uint64_t fmask = 0;
-    double rinv[RPL];
+    double *Kx = Kimg + GP<MAXM>::XOFF;   // L_jj | RN(1/L_jj) | z | (spare)
+    // the forward solve L z = y (models.py:90, inner solve_triangular) runs fused into the
+    // columns: z_j needs row j's accumulator after columns 0..j-1 -- exactly when column j
+    // finishes -- so it is formed there, with column j's L_jj / RN(1/L_jj) still in registers
+    double acc[RPL];
 #pragma unroll
-    for (int s = 0; s < RPL; s++) {
-        diag[s] = 1.0;
-        rinv[s] = 1.0;
-    }
+    for (int s = 0; s < RPL; s++) acc[s] = y[s];
     // OpenBLAS dpotf2_L's sums (the reference's LAPACK; oracle potf2_dot / potf2_gemv_row):
     //   pivot   a_jj - ddot(row j): accumulators t1/t2 over groups of 4, fma(x0,x0,x2^2) etc.;
     //   below   "vector rows" (the first ((m-1-j) & -4) rows under j): y -= 4-column fma chains,
@@ -316,10 +322,10 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
             ljj = sqrt(piv);
             ri = 1.0 / ljj;
         }
-        diag[SJ] = (lo == LJ) ? ljj : diag[SJ];
-        rinv[SJ] = (lo == LJ) ? ri : rinv[SJ];
+        Kx[j] = ljj;
+        Kx[MAXM + j] = ri;
         // (the owner's diagonal entry a[SJ][j] becomes t*ri too: nothing reads it -- the solves
-        // take L_jj from diag[], and the row-j updates they make after capturing z_j / alpha_j are
+        // take L_jj from Kx, and the row-j updates they make after capturing z_j / alpha_j are
         // the harmless ones noted there)
 #pragma unroll
         for (int s = 0; s < RPL; s++)
@@ -328,6 +334,18 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
 #pragma unroll
             for (int s = 0; s < RPL; s++)
                 if (16 * (s + 1) > j) asm volatile("" : "+v"(a[s][j]));
+        }
+        // forward-solve step j: z_j = acc_j / L_jj (Markstein: x * RN(1/L_jj), corrected; every
+        // lane divides the broadcast accumulator by the row's L_jj, bitwise the row owner doing it),
+        // then the rows below subtract L_ij z_j (rows <= j update harmlessly)
+        {
+            const double zb = row_bcast<LJ>(acc[SJ]);
+            const double q = zb * ri;
+            const double zj = fma(fma(-q, ljj, zb), ri, q);
+            Kx[2 * MAXM + j] = zj;
+#pragma unroll
+            for (int s = 0; s < RPL; s++)
+                if (16 * (s + 1) > j + 1) acc[s] = acc[s] - a[s][j] * zj;
         }
         // a finished 4-column block: fold it into the carried ddot of every set with rows past j
         if constexpr (j % 4 == 3) {
@@ -344,28 +362,9 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
         for (int s = 0; s < RPL; s++) alpha[s] = 0.0;
         return false;
     }
-    // x / L_ii for this lane's row of set s: Markstein-corrected x * RN(1/L_ii) (= IEEE x/L_ii)
-    auto divd = [&](int s, double x) {
-        const double q = x * rinv[s];
-        return fma(fma(-q, diag[s], x), rinv[s], q);
-    };
-    // 4) forward solve L z = y (models.py:90, inner solve_triangular); rows <= i update
-    //    harmlessly (their z is already captured)
-    double acc[RPL], z[RPL];
-#pragma unroll
-    for (int s = 0; s < RPL; s++) {
-        acc[s] = y[s];
-        z[s] = 0.0;
-    }
-    static_for<0, MAXM>([&](auto ic) {
-        constexpr int i = decltype(ic)::value, SI = i / 16, LI = i % 16;
-        const double zi = row_bcast<LI>(divd(SI, acc[SI]));
-        z[SI] = (lo == LI) ? zi : z[SI];
-#pragma unroll
-        for (int s = 0; s < RPL; s++)
-            if (16 * (s + 1) > i + 1) acc[s] = acc[s] - a[s][i] * zi;
-    });
-    // 5) back solve L^T alpha = z: L to the LDS image, column of this lane's row(s) back
+    // 5) back solve L^T alpha = z: L to the LDS image, column of this lane's row(s) back.  L_ii
+    //    and RN(1/L_ii) come from the scalar slots (no LDS store in this loop, so LLVM issues
+    //    those reads ahead of the chain); alpha_i stays with its row owner by a select.
     wave_lds_sync();
 #pragma unroll
     for (int s = 0; s < RPL; s++) {
@@ -383,15 +382,23 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
         }
     }
     wave_lds_sync();
+    // this lane's z and L_ii (rows past MAXM: the pad's exact 0 and 1)
     double acc2[RPL];
 #pragma unroll
     for (int s = 0; s < RPL; s++) {
-        acc2[s] = z[s];
+        const int row = l + 16 * s;
+        const bool in = 16 * (s + 1) <= MAXM || row < MAXM;
+        const int r = min(row, MAXM - 1);
+        acc2[s] = in ? Kx[2 * MAXM + r] : 0.0;
+        diag[s] = in ? Kx[r] : 1.0;
         alpha[s] = 0.0;
     }
     static_for<0, MAXM>([&](auto ic) {
         constexpr int i = MAXM - 1 - decltype(ic)::value, SI = i / 16, LI = i % 16;
-        const double ai = row_bcast<LI>(divd(SI, acc2[SI]));
+        const double ab = row_bcast<LI>(acc2[SI]);
+        const double li = Kx[i], ri = Kx[MAXM + i];
+        const double q = ab * ri;
+        const double ai = fma(fma(-q, li, ab), ri, q);   // ab / L_ii, as the forward step
         alpha[SI] = (lo == LI) ? ai : alpha[SI];
 #pragma unroll
         for (int s = 0; s < RPL; s++)

@@ -25,6 +25,17 @@ struct MathC {
     static constexpr double EXP_UNF = -745.1332191019412;
 };
 
+// fma(a, b, c) as one 3-address v_fma_f64.  In a Horner step p = fma(p, r, C) with C a
+// loop-invariant coefficient held in a VGPR (gfx950's VOP3 takes no 64-bit literal, and the
+// SGPRs are taken), LLVM emits the 2-address v_fmac_f64, whose addend is its destination, and so
+// first copies C there: a v_mov_b64 per step, ~130 per likelihood evaluation at m = 20.  Same
+// operation, same bits.
+__device__ __forceinline__ double fma3(double a, double b, double c) {
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
 // exp(hi + lo) with |lo| << |hi|.  Branch-free (selects) so it inlines cheaply inside the
 // unrolled kernel-row loops; identical results to the oracle's branchy form.
 // NONPOS: hi <= 0 or NaN, lo == 0 (the SE kernel's c*D2 with c < 0 <= D2, models.py:146-148) --
@@ -40,16 +51,16 @@ __device__ __forceinline__ double nn_exp_t(double hi, double lo) {
     if constexpr (!NONPOS) r = r + lo;
     // sum_{j=0}^{13} r^j / j!
     double p = 1.0 / 6227020800.0;             // 1/13!
-    p = fma(p, r, 1.0 / 479001600.0);          // 1/12!
-    p = fma(p, r, 1.0 / 39916800.0);
-    p = fma(p, r, 1.0 / 3628800.0);
-    p = fma(p, r, 1.0 / 362880.0);
-    p = fma(p, r, 1.0 / 40320.0);
-    p = fma(p, r, 1.0 / 5040.0);
-    p = fma(p, r, 1.0 / 720.0);
-    p = fma(p, r, 1.0 / 120.0);
-    p = fma(p, r, 1.0 / 24.0);
-    p = fma(p, r, 1.0 / 6.0);
+    p = fma3(p, r, 1.0 / 479001600.0);         // 1/12!
+    p = fma3(p, r, 1.0 / 39916800.0);
+    p = fma3(p, r, 1.0 / 3628800.0);
+    p = fma3(p, r, 1.0 / 362880.0);
+    p = fma3(p, r, 1.0 / 40320.0);
+    p = fma3(p, r, 1.0 / 5040.0);
+    p = fma3(p, r, 1.0 / 720.0);
+    p = fma3(p, r, 1.0 / 120.0);
+    p = fma3(p, r, 1.0 / 24.0);
+    p = fma3(p, r, 1.0 / 6.0);
     p = fma(p, r, 0.5);
     p = fma(p, r, 1.0);
     p = fma(p, r, 1.0);
@@ -216,12 +227,11 @@ __device__ __forceinline__ double nn_sin_pi(double x) {
     const double s = fma(r * z, p, r);
     // (-1)^n: the low bit of n + 1.5*2^52 (n in two's complement for |n| < 2^51), into the sign
     const long long par = __double_as_longlong(n + 6755399441055744.0) & 1;
-    const double sg = __longlong_as_double(__double_as_longlong(s) ^ (par << 63));
-#ifdef NNGP_RK_FMA
-    return sg;   // contracted build: inf/NaN already give NaN (r = NaN)
-#else
-    return (x - x == 0.0) ? sg : x - x;   // NaN for inf / NaN arguments, as sin
-#endif
+    // inf / NaN arguments give NaN without a select, as sin does: n = rint(+-inf / pi) = +-inf, so
+    // r = fma(-n, PI_1, x) = inf - inf = NaN (a NaN x propagates).  Finite x never takes the
+    // select the round-2 form had (x - x == 0), so finite results are unchanged; only the NaN's
+    // payload differs (4 VALU per sine, 16 per ThomasLabyrinth RK4 step)
+    return __longlong_as_double(__double_as_longlong(s) ^ (par << 63));
 }
 
 __device__ __forceinline__ double nn_sin(double x) {

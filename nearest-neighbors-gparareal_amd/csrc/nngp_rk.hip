@@ -444,14 +444,15 @@ template <int S> struct FhnPairImages {
     static constexpr int of(int s) { return (S % 2 == 1 && s == S - 1) ? 2 : (s & 1); }
 };
 
-// ((a L)@v)_p as fhn_lap, the five coefficients selected once per thread
-__device__ __forceinline__ double fhn_lap5(const double *__restrict__ V, const Nbr5 &nb, double k0, double k1,
-                                           double k2, double k3, double k4) {
-    double s = k0 * V[nb.c0];
-    s = s + k1 * V[nb.c1];
-    s = s + k2 * V[nb.c2];
-    s = s + k3 * V[nb.c3];
-    s = s + k4 * V[nb.c4];
+// ((a L)@v)_p as fhn_lap, from the five neighbour values (ascending column order) and the five
+// coefficients selected once per thread
+__device__ __forceinline__ double fhn_sum5(const double (&v)[5], double k0, double k1, double k2, double k3,
+                                           double k4) {
+    double s = k0 * v[0];
+    s = s + k1 * v[1];
+    s = s + k2 * v[2];
+    s = s + k3 * v[3];
+    s = s + k4 * v[4];
     return s;
 }
 
@@ -495,25 +496,39 @@ __global__ void __launch_bounds__(1024) rk_fhn_pair_kernel(FieldArgs fa, int n_s
     const int64_t j0 = j0s ? j0s[slice] : 0;
     LinGrid grid;
     if constexpr (LINSPACE) grid.init(j0, gsteps, T0, dt);
+    // stage 0's input is u itself (RK.py:153-166: no a_0j terms)
+    double xw[2];
+#pragma unroll
+    for (int r = 0; r < 2; r++) xw[r] = NORM ? (u[r] + 1) * w[r] + mn[r] : u[r];
     for (int64_t n = 0; n < steps; n++) {
         const double h = LINSPACE ? grid.next(n, T0, T1, dt) : dt;
+        double acc[2];   // sum_s b_s k_s, accumulated as the stages finish (step_update's order)
 #pragma unroll
         for (int s = 0; s < S; s++) {
             const int img = (S == 1) ? (int)(n & 1) : IM::of(s);
             double *V = smem + img * 2 * PS;
-            double xw[2];
 #pragma unroll
-            for (int r = 0; r < 2; r++) {
-                const double x = stage_input<T, 2>(s, u[r], k, r);
-                xw[r] = NORM ? (x + 1) * w[r] + mn[r] : x;
-                V[p + r * PS] = xw[r];
-            }
+            for (int r = 0; r < 2; r++) V[p + r * PS] = xw[r];
             __syncthreads();
+            double va[5], vb[5];
+            va[0] = V[nb.c0]; va[1] = V[nb.c1]; va[2] = V[nb.c2]; va[3] = V[nb.c3]; va[4] = V[nb.c4];
+            vb[0] = V[PS + nb.c0]; vb[1] = V[PS + nb.c1]; vb[2] = V[PS + nb.c2]; vb[3] = V[PS + nb.c3];
+            vb[4] = V[PS + nb.c4];
+            // the next stage's input terms that do not involve this stage's k, computed while the
+            // neighbour reads are in flight (pinned before the stencil: the reads' results pass
+            // through the same empty asm, so LLVM can neither sink these sums past the stencil
+            // nor start the stencil before them; profiles/r03: 47 % of a 64-slice step's wave
+            // cycles were spent waiting, mostly on these reads and the barrier)
+            double pn[2] = {0.0, 0.0};
+            if (s + 1 < S) {
+#pragma unroll
+                for (int r = 0; r < 2; r++) pn[r] = stage_partial<T, 2>(s + 1, k, r);
+            }
             // systems.py:365-366, as rk_field_kernel with V[e] / V[half+e] / V[e-half] in registers
-            const double lu = fhn_lap5(V, nb, ka0, ka1, ka2, ka3, ka4);
+            const double lu = fhn_sum5(va, ka0, ka1, ka2, ka3, ka4);
             const double u1 = xw[0], u1c = u1 * (u1 * u1);
             double fu = (((lu + u1) - u1c) - xw[1]) + -5E-3 * 1.0;
-            const double lv = fhn_lap5(V + PS, nb, kb0, kb1, kb2, kb3, kb4);
+            const double lv = fhn_sum5(vb, kb0, kb1, kb2, kb3, kb4);
             double fv = (1 / 0.1) * ((lv + xw[0]) - xw[1]);
             if (NORM) {
                 fu = fu * sc[0];
@@ -521,9 +536,20 @@ __global__ void __launch_bounds__(1024) rk_fhn_pair_kernel(FieldArgs fa, int n_s
             }
             k[s * 2 + 0] = h * fu;
             k[s * 2 + 1] = h * fv;
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+                step_accumulate<T>(s, acc[r], k[s * 2 + r]);   // RK.py:170, in its order
+                if (s + 1 < S) {
+                    const double x = stage_finish<T, 2>(s + 1, u[r], pn[r], k, r);
+                    xw[r] = NORM ? (x + 1) * w[r] + mn[r] : x;
+                }
+            }
         }
 #pragma unroll
-        for (int r = 0; r < 2; r++) u[r] = step_update<T, 2>(u[r], k, r);   // RK.py:170
+        for (int r = 0; r < 2; r++) {
+            u[r] = u[r] + acc[r];   // RK.py:170
+            xw[r] = NORM ? (u[r] + 1) * w[r] + mn[r] : u[r];
+        }
     }
     if (ok) {
         uF[(size_t)slice * d + p] = u[0];

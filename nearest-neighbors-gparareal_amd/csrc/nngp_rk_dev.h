@@ -127,6 +127,52 @@ __device__ __forceinline__ double stage_input(int s, double u, const double *k, 
     return first ? u : u + t;
 }
 
+// stage_input split at j = s - 1, for kernels that form the terms not involving k_{s-1} early:
+// stage_partial = the sum over the non-zero a_sj with j < s - 1 (0.0 if none), stage_finish adds
+// a_{s,s-1} k_{s-1} and u -- the same additions in the same order as stage_input.
+template <typename T>
+__host__ __device__ constexpr bool stage_has_partial(int s) {
+    for (int j = 0; j + 1 < s; j++)
+        if (T::A[s][j] != 0.0) return true;
+    return false;
+}
+template <typename T, int KS>
+__device__ __forceinline__ double stage_partial(int s, const double *k, int c) {
+    double t = 0.0;
+    bool first = true;
+#pragma unroll
+    for (int j = 0; j < T::S; j++) {
+        if (j + 1 >= s || T::A[s][j] == 0.0) continue;
+        const double v = T::A[s][j] * k[j * KS + c];
+        t = first ? v : t + v;
+        first = false;
+    }
+    return t;
+}
+template <typename T, int KS>
+__device__ __forceinline__ double stage_finish(int s, double u, double partial, const double *k, int c) {
+    const bool hp = stage_has_partial<T>(s), hl = s >= 1 && T::A[s][s - 1] != 0.0;
+    if (!hp && !hl) return u;
+    double t = partial;
+    if (hl) {
+        const double v = T::A[s][s - 1] * k[(s - 1) * KS + c];
+        t = hp ? t + v : v;
+    }
+    return u + t;
+}
+// step_update accumulated stage by stage: acc after stage s (the same order, non-zero b_s only;
+// acc is unset until the first non-zero b_s, which every tableau has at s = 0 or 1)
+template <typename T>
+__device__ __forceinline__ void step_accumulate(int s, double &acc, double ks) {
+    if (T::B[s] == 0.0) return;
+    bool first = true;
+#pragma unroll
+    for (int j = 0; j < T::S; j++)
+        if (j < s && T::B[j] != 0.0) first = false;
+    const double v = T::B[s] * ks;
+    acc = first ? v : acc + v;
+}
+
 // u + sum_s b_s k_s over the non-zero b_s in ascending s (jnp.sum(b*k, 1), RK.py:170)
 template <typename T, int KS>
 __device__ __forceinline__ double step_update(double u, const double *k, int c) {

@@ -634,8 +634,7 @@ static const double SP_S1 = -0x1.5555555555555p-3, SP_S2 = 0x1.11111111110c1p-7,
                     SP_S4 = 0x1.71de3a5287c12p-19, SP_S5 = -0x1.ae6454cb54cccp-26, SP_S6 = 0x1.6123cb28741dap-33,
                     SP_S7 = -0x1.ae431d76c3814p-41, SP_S8 = 0x1.88299fb2db5f9p-49;
 
-double nn_sin_pi(double x) {
-    const int fin = (x - x) == 0.0;
+double nn_sin_pi(double x) {   /* inf / NaN: n = +-inf or NaN, so r = NaN and the result is NaN */
     const double n = rint(x * SP_INVPI);
     double r = fma(-n, SP_PI_1, x);
     r = fma(-n, SP_PI_2, r);
@@ -655,7 +654,7 @@ double nn_sin_pi(double x) {
     memcpy(&sb, &s, sizeof sb);
     sb ^= (nb & 1u) << 63;
     memcpy(&s, &sb, sizeof s);
-    return fin ? s : x - x;
+    return s;
 }
 
 double nn_sin(double x) {
