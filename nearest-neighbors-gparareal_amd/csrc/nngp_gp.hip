@@ -1127,6 +1127,161 @@ __global__ void __launch_bounds__(WGT<MAXM>::T) nm_spec_kernel(NMArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Two-level speculative Nelder-Mead: W waves (4 W rows) per fit, for few fits (a latency-bound
+// correction: the slowest fit's chain of rounds is the correction's time).  Rows 0-3 take the
+// one-level candidates above; while the request is a reflection from a finite simplex, rows 4..
+// also take the NEXT iteration's reflection, expansion and both contractions for the likeliest
+// outcomes of this one, each of which fixes the sorted simplex the next centroid is formed from:
+//   set 1 (W >= 2): the reflection is accepted between the best and the middle vertex
+//                   (f0 <= f(r) < f1: simplex s0, r, s1);
+//   set 2 (W == 4): the inside contraction is accepted and is the new best (s_ic, s0, s1);
+//   set 3 (W == 4): the inside contraction is accepted and stays the worst (s0, s1, s_ic).
+// (Outcome frequencies on trajectory-like fits, tools/_nm_spec_sim.py: reflection accepted 21 %,
+// inside contraction 19-20 % best / 16-21 % worst, expansions 25-30 %.)  The candidates are formed
+// with nm_check's own expressions, and the unchanged state machine consumes whatever was
+// requested and answered, so a fit is bitwise the one-level kernel's (and scipy's); only requested
+// points count towards nfev.  Simulated on those fits: the slowest fit's rounds 50 -> 28 (W = 4),
+// 50 -> 36 (W = 2).  A round's candidates and values go through LDS; every wave of a fit runs the
+// state machine redundantly on the same values.
+// ---------------------------------------------------------------------------------------------
+struct NMCand2 {
+    double x, y, f;
+    int st;
+};
+
+// the next iteration's candidates after p replaces the worst vertex and sorts to `rank` among
+// (s0, s1) -- nm_end_iter + nm_check's expressions for that simplex
+__device__ __forceinline__ void nm_next_set(const NM &S, double px, double py, int rank, NMCand2 *c) {
+    double ax = S.s0x, ay = S.s0y, bx = S.s1x, by = S.s1y, wx = px, wy = py;   // rank 2
+    if (rank == 0) { ax = px; ay = py; bx = S.s0x; by = S.s0y; wx = S.s1x; wy = S.s1y; }
+    else if (rank == 1) { ax = S.s0x; ay = S.s0y; bx = px; by = py; wx = S.s1x; wy = S.s1y; }
+    const double xbx = (ax + bx) / 2, xby = (ay + by) / 2;
+    c[0] = NMCand2{2 * xbx - 1 * wx, 2 * xby - 1 * wy, 0.0, ST_REFLECT};
+    c[1] = NMCand2{3 * xbx - 2 * wx, 3 * xby - 2 * wy, 0.0, ST_EXPAND};
+    c[2] = NMCand2{1.5 * xbx - 0.5 * wx, 1.5 * xby - 0.5 * wy, 0.0, ST_CONTRACT};
+    c[3] = NMCand2{0.5 * xbx + 0.5 * wx, 0.5 * xby + 0.5 * wy, 0.0, ST_ICONTRACT};
+}
+
+// this row's candidate (slot 0 .. 4W-1; st = -1: none).  Every lane forms all sets from the
+// fit's (uniform) state and keeps its own slot's with static selects: a few dozen VALU per round
+// against a likelihood evaluation's ~2 500, and no serial hand-off through one lane.
+template <int W>
+__device__ __forceinline__ NMCand2 nm_candidate_slot(const NM &S, int slot) {
+    NMCand l1[4];
+    nm_candidates(S, l1);
+    NMCand2 c{S.px, S.py, 0.0, -1};
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (slot == k) c = NMCand2{l1[k].x, l1[k].y, 0.0, l1[k].st};
+    if (W == 1) return c;
+    const bool lv2 = S.st == ST_REFLECT && !(S.f0 == INFINITY && S.f1 == INFINITY && S.f2 == INFINITY);
+    if (!lv2 || slot < 4) return c;
+    NMCand2 set[4];
+    const int si = slot / 4;   // 1: reflection accepted (rank 1); 2 / 3: inside contraction best / worst
+    const double xi = 0.5 * S.xbx + 0.5 * S.s2x, yi = 0.5 * S.xby + 0.5 * S.s2y;   // ST_ICONTRACT's point
+    nm_next_set(S, si == 1 ? S.xrx : xi, si == 1 ? S.xry : yi, si == 1 ? 1 : (si == 2 ? 0 : 2), set);
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if ((slot & 3) == k) c = set[k];
+    return c;
+}
+
+template <int MAXM, int W>
+__global__ void __launch_bounds__(256) nm_spec2_kernel(NMArgs a) {
+    constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG, FPW = 4 / W;   // fits per workgroup
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    __shared__ NMCand2 sC[FPW][4 * W];   // the round's candidates and their values, per fit
+    if (a.skip && *a.skip) return;   // uniform: the whole grid exits (speculation hit)
+    nm_batch_offsets(a);
+    const int m = a.m;
+    const int nfc = a.nj * a.R;
+    double *sD2 = sm;
+    double *sK = sD2 + m * m;                           // [16][IMG]
+    const int tid = threadIdx.x, wv = tid / 64;
+    const int g = (tid & 63) / 16, l = tid % 16;
+    const int fs = wv / W;                              // this wave's fit within the workgroup
+    const int slot = (wv % W) * 4 + g;                  // this row's candidate slot
+    int f = blockIdx.x * FPW + fs;
+    for (int i = tid; i < m * m; i += blockDim.x) sD2[i] = a.D2[i];
+    bool live = true;
+    if (a.resume) {
+        if (f >= *a.park_count) live = false;
+        else f = a.park_list[f];
+    } else if (f >= a.n_fits) {
+        live = false;
+    }
+    const int fc = live ? f : 0;
+    int coord, jidx;
+    if (a.coord) {
+        coord = a.coord[fc];
+        jidx = a.jitter_idx[fc];
+    } else {   // product(coord, jitter, restart) order (models.py:186)
+        coord = fc / nfc;
+        jidx = (fc % nfc) / a.R;
+    }
+    double y[RPL];
+#pragma unroll
+    for (int s = 0; s < RPL; s++) {
+        const int row = l + 16 * s;
+        y[s] = (row < m) ? a.Y[(int64_t)coord * a.ys_c + (int64_t)row * a.ys_r] : 0.0;
+    }
+    const double jit = jit_lookup(a, jidx);
+    double *Kimg = sK + (size_t)(tid / 16) * IMG;
+    GPLane<MAXM> P;
+    gp_lane_init<MAXM>(P, m, l);
+    gp_image_init<MAXM>(Kimg, m, l);
+
+    NMCfg cfg{a.fatol, a.xatol, a.maxfev, a.maxfev};
+    NM St;
+    if (!live) {
+        St.st = ST_DONE;
+    } else if (a.resume) {
+        St = a.park[f];
+    } else {
+        const double t0x = a.theta0[2 * f], t0y = a.theta0[2 * f + 1];
+        St.f0 = St.f1 = St.f2 = INFINITY;
+        St.xbx = St.xby = St.xrx = St.xry = St.fxr = 0.0;
+        nm_start(St, cfg, t0x, t0y);
+    }
+    // workgroup-uniform rounds (a finished fit's rows evaluate a dummy point until all are done)
+    const int lane = tid & 63;
+    while (__syncthreads_or(St.st != ST_DONE)) {
+        const bool run = St.st != ST_DONE;   // uniform over the fit's waves
+        const NMCand2 mine = run ? nm_candidate_slot<W>(St, slot) : NMCand2{-1.0, -1.0, 0.0, -1};
+        // unused slots evaluate the request itself (a duplicate; never matched)
+        const double fv = gp_nlml<MAXM>(m, l, P, sD2, mine.st >= 0 ? mine.x : St.px,
+                                        mine.st >= 0 ? mine.y : St.py, jit, y, Kimg);
+        if (l == 0) sC[fs][slot] = NMCand2{mine.x, mine.y, fv, mine.st};
+        __syncthreads();
+        // consume every answered request in scipy's order: lane k < 4W holds candidate k; the
+        // lowest matching slot answers (the order a sequential scan would take)
+        const NMCand2 ck = sC[fs][lane < 4 * W ? lane : 0];
+        uint64_t used = 0;
+        while (run && St.st != ST_DONE) {
+            const bool match = lane < 4 * W && !((used >> lane) & 1) && ck.st == St.st && ck.x == St.px &&
+                               ck.y == St.py;
+            const uint64_t mk = __builtin_amdgcn_ballot_w64(match);
+            if (!mk) break;
+            const int hit = __builtin_ctzll(mk);
+            used |= 1ull << hit;
+            nm_consume(St, cfg, wave_lane_double(ck.f, hit));
+        }
+    }
+    if (live && (tid & (64 * W - 1)) == 0) {
+        const double fval = (St.f1 != St.f1 || St.f2 != St.f2) ? NAN : St.f0;
+        if (a.theta_out) { a.theta_out[2 * f] = St.s0x; a.theta_out[2 * f + 1] = St.s0y; }
+        if (a.fval_out) a.fval_out[f] = fval;
+        if (a.nfev_out) a.nfev_out[f] = St.fcalls;
+        if (a.fits_out) {
+            a.fits_out[4 * f + 0] = St.s0x;
+            a.fits_out[4 * f + 1] = St.s0y;
+            a.fits_out[4 * f + 2] = fval;
+            a.fits_out[4 * f + 3] = (double)St.fcalls;
+        }
+    }
+}
+
 // posterior mean per coordinate, one 16-lane group per coordinate (models.py:162-168, 217).
 // (theta, jitter) either given (a.theta0[c], a.jitter_idx[c]: nngp_gp_mean) or the first arg-min
 // of the coordinate's a.nj*a.R fits in a.fits_out (the unfused nngp_predict path, used when a
@@ -1536,10 +1691,37 @@ static int run_mean(NMArgs &a, hipStream_t st) {
 
 // speculative kernel: one wave per fit, 4 fits per 256-thread workgroup (1 per 64-thread
 // workgroup for m > 32)
+// waves per fit of the two-level kernel for a launch of `total` fits: 4 while every fit's four
+// waves get a SIMD of their own (total <= #CU), 2 up to twice that, else the one-level kernel.
+// Resumed (parked) fits keep one wave each: their count is only known on the device.
+// NNGP_NM_LEVEL2=0 disables it.
+static int spec_waves(int total, int maxm, bool resume) {
+    const int e = env_int("NNGP_NM_LEVEL2", 1);
+    if (maxm > 32 || resume || e == 0) return 1;
+    if (e == 2 || e == 4) return e;   // forced (measurements)
+    static int ncu = 0;
+    if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) ncu = 256;
+    if (ncu <= 0) ncu = 256;
+    return total <= ncu ? 4 : (total <= 2 * ncu ? 2 : 1);
+}
+
 static int run_nm_spec(NMArgs &a, hipStream_t st, int nq = 1) {
     const int maxm = maxm_for(a.m);
     const int threads = wg_threads(maxm);
     const size_t lds = sizeof(double) * ((size_t)a.m * a.m + (size_t)(threads / 16) * k_image_doubles(maxm));
+    const int W = spec_waves(a.n_fits * nq, maxm, a.resume != 0);
+    if (W > 1) {
+        const dim3 grid2((a.n_fits + 4 / W - 1) / (4 / W), nq);
+        return with_maxm(a.m, [&](auto mc) {
+            constexpr int M = decltype(mc)::value;
+            if constexpr (M <= 32) {
+                if (W == 4) hipLaunchKernelGGL((nm_spec2_kernel<M, 4>), grid2, dim3(256), lds, st, a);
+                else hipLaunchKernelGGL((nm_spec2_kernel<M, 2>), grid2, dim3(256), lds, st, a);
+                NNGP_LAUNCH_CHECK();
+            }
+            return NNGP_OK;
+        });
+    }
     const dim3 grid((a.n_fits + threads / 64 - 1) / (threads / 64), nq);
     return with_maxm(a.m, [&](auto mc) {
         hipLaunchKernelGGL(nm_spec_kernel<decltype(mc)::value>, grid, dim3(threads), lds, st, a);

@@ -299,6 +299,7 @@ def test_predict_restarts_and_small_training_set(gpu):
 
 @pytest.mark.parametrize('park', ['0', '30', '100'])
 @pytest.mark.parametrize('m,d,R', [(5, 3, 1), (12, 4, 2), (16, 3, 2), (17, 5, 2), (19, 7, 1), (20, 6, 1), (20, 3, 2), (30, 2, 2),
+                                   (15, 40, 1),
                                    (10, 300, 1), (18, 130, 2), (20, 80, 1), (24, 3, 1),
                                    (40, 3, 1), (48, 4, 2), (64, 3, 1), (56, 40, 1), (33, 140, 1)])
 def test_predict_every_padded_size_and_fallback_vs_oracle(gpu, m, d, R, park, monkeypatch):
@@ -309,7 +310,9 @@ def test_predict_every_padded_size_and_fallback_vs_oracle(gpu, m, d, R, park, mo
     when a coordinate's fits exceed a workgroup (m=18, R=2 at d=130: 4 680 fits), as fits +
     arg-min/mean kernels.  With the tail hand-off (NNGP_NM_PARK = cap > 0) the packed kernel
     parks every fit still running at `cap` evaluations and the speculative kernel resumes it
-    (cap 30 parks most fits).  Every path is bitwise the oracle."""
+    (cap 30 parks most fits).  Up to #CU fits a fit gets four waves and up to twice that two (the
+    two-level speculation: the next iteration's candidates for the likeliest outcomes; m=15 d=40:
+    360 fits, two waves).  Every path is bitwise the oracle."""
     import torch
     monkeypatch.setenv('NNGP_NM_PARK', park)
     rng = np.random.default_rng(m * 10 + d + R)

@@ -49,6 +49,15 @@ if __name__ == '__main__':
             for d in ds:
                 case(d, m, 1, 1500)
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == 'level2':
+        # latency-bound corrections (run with NNGP_NM_LEVEL2=0 / 1 / 2 / 4)
+        case(3, 15, 2, 600)
+        case(3, 10, 1, 600)
+        case(2, 15, 2, 600)
+        case(20, 20, 1, 1500)
+        case(40, 15, 1, 1500)
+        case(100, 20, 1, 3000)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == 'park':
         # packed-kernel shapes (run with NNGP_NM_PARK=0 / 60 / 100 / 150)
         case(256, 15, 1, 1500)
