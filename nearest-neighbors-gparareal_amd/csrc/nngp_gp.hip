@@ -1137,7 +1137,7 @@ __global__ void __launch_bounds__(WGT<MAXM>::T) nm_spec_kernel(NMArgs a) {
 //                   (f0 <= f(r) < f1: simplex s0, r, s1);
 //   set 2 (W == 4): the inside contraction is accepted and is the new best (s_ic, s0, s1);
 //   set 3 (W == 4): the inside contraction is accepted and stays the worst (s0, s1, s_ic).
-// (Outcome frequencies on trajectory-like fits, tools/_nm_spec_sim.py: reflection accepted 21 %,
+// (Outcome frequencies on trajectory-like fits, tests/nm_spec_sim.py: reflection accepted 21 %,
 // inside contraction 19-20 % best / 16-21 % worst, expansions 25-30 %.)  The candidates are formed
 // with nm_check's own expressions, and the unchanged state machine consumes whatever was
 // requested and answered, so a fit is bitwise the one-level kernel's (and scipy's); only requested
