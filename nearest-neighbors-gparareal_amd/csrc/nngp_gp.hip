@@ -772,8 +772,11 @@ struct NMArgs {
     int32_t *queue;
     // tail hand-off (single prediction): the packed kernel parks a fit whose evaluation count
     // reaches park_cap (its Nelder-Mead state, pending request included, in park[f], f appended to
-    // park_list); the speculative kernel then resumes the parked fits (resume != 0), a wave each
-    int park_cap, resume;
+    // park_list); the speculative kernels then resume the parked fits (resume != 0).  park_count[0]
+    // finite fits sit at the front of park_list, park_count[1] all-+inf ones at its back.  The
+    // two-level resume (nm_spec2_kernel<M, 0>) gives a finite fit 4 waves while their count is
+    // <= resume_w4, 2 while <= resume_w2, else 1; an all-+inf fit one
+    int park_cap, resume, resume_w4, resume_w2;
     // unfused fits in product order (coord null): rows take fits jitter-major (slot s -> fit
     // (s % d) * nfc + s / d), so a wave's rows share a jitter (and, for R = 1, differ in the
     // coordinate only); the kernel matrix K depends on (theta, jitter), not on the coordinate
@@ -941,9 +944,14 @@ __global__ void __launch_bounds__(NMBound<MAXM>::T) nm_fit_kernel(NMArgs a) {
                 // a long fit: park it (state with its pending request) for the speculative kernel,
                 // which finishes it a wave per fit in ~1.5x fewer rounds, so this wave's tail does
                 // not set the launch's length (uniform within the group)
+                // (finite simplices from the front of park_list, all-+inf ones -- which run to
+                // maxfev -- from the back: the resume gives them different shapes)
                 if (l == 0) {
                     a.park[f] = St;
-                    a.park_list[atomicAdd(a.park_count, 1)] = f;
+                    if (St.f0 == INFINITY && St.f1 == INFINITY && St.f2 == INFINITY)
+                        a.park_list[a.n_fits - 1 - atomicAdd(a.park_count + 1, 1)] = f;
+                    else
+                        a.park_list[atomicAdd(a.park_count, 1)] = f;
                 }
                 parked = true;
                 St.st = ST_DONE;
@@ -1041,8 +1049,9 @@ __global__ void __launch_bounds__(WGT<MAXM>::T) nm_spec_kernel(NMArgs a) {
     for (int i = tid; i < m * m; i += blockDim.x) sD2[i] = a.D2[i];
     __syncthreads();
     if (a.resume) {                                      // the parked fits of the packed kernel
-        if (f >= *a.park_count) return;
-        f = a.park_list[f];
+        const int nf = a.park_count[0];                  // finite ones first, then the all-+inf
+        if (f >= nf + a.park_count[1]) return;
+        f = f < nf ? a.park_list[f] : a.park_list[a.n_fits - 1 - (f - nf)];
     } else if (f >= a.n_fits) {
         return;                                          // whole wave exits together
     }
@@ -1166,9 +1175,25 @@ __device__ __forceinline__ void nm_next_set(const NM &S, double px, double py, i
 // this row's candidate (slot 0 .. 4W-1; st = -1: none).  Every lane forms all sets from the
 // fit's (uniform) state and keeps its own slot's with static selects: a few dozen VALU per round
 // against a likelihood evaluation's ~2 500, and no serial hand-off through one lane.
-template <int W>
-__device__ __forceinline__ NMCand2 nm_candidate_slot(const NM &S, int slot) {
+__device__ __forceinline__ NMCand2 nm_candidate_slot(const NM &S, const NMCfg &cfg, int slot, int W) {
     NMCand l1[4];
+    if (W > 1 && slot >= 4 && S.st == ST_REFLECT && S.f0 == INFINITY && S.f1 == INFINITY && S.f2 == INFINITY) {
+        // an all-+inf simplex (the fits that run to maxfev: the parked tail of a large correction):
+        // wave w of the fit takes iteration w's requests as the state machine makes them if every
+        // earlier request is +inf too -- it answers them on a copy with +inf (reflection, inside
+        // contraction, both shrink points per iteration), so W iterations per round instead of one
+        NM T = S;
+        const int w = slot / 4;   // uniform over the wave
+        for (int k = 0; k < 4 * w; k++)
+            if (T.st != ST_DONE) nm_consume(T, cfg, INFINITY);
+        NMCand2 c{S.px, S.py, 0.0, -1};
+        if (T.st == ST_DONE) return c;
+        const int nc = nm_candidates(T, l1);
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if ((slot & 3) == k && k < nc) c = NMCand2{l1[k].x, l1[k].y, 0.0, l1[k].st};
+        return c;
+    }
     nm_candidates(S, l1);
     NMCand2 c{S.px, S.py, 0.0, -1};
 #pragma unroll
@@ -1187,30 +1212,51 @@ __device__ __forceinline__ NMCand2 nm_candidate_slot(const NM &S, int slot) {
     return c;
 }
 
+// W = 0: the resume of the packed kernel's parked fits, shapes chosen on the device from the
+// parked counts -- the finite fits' workgroups first (4 waves per fit while they number <=
+// resume_w4, 2 while <= resume_w2, else 1), then the all-+inf fits' (a wave each: one iteration
+// is one round for them already, and their waves would only take issue slots from the finite
+// chains); the grid covers the largest case and the rest of it exits at once.
 template <int MAXM, int W>
 __global__ void __launch_bounds__(256) nm_spec2_kernel(NMArgs a) {
-    constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG, FPW = 4 / W;   // fits per workgroup
+    constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG;
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    __shared__ NMCand2 sC[FPW][4 * W];   // the round's candidates and their values, per fit
+    __shared__ NMCand2 sC[16];   // the round's candidates and their values: fit fs's at [4*Wr*fs, 4*Wr*(fs+1))
     if (a.skip && *a.skip) return;   // uniform: the whole grid exits (speculation hit)
+    const int tid = threadIdx.x, wv = tid / 64;
+    int Wr = W, f = 0;
+    bool live = true;
+    if (W == 0) {
+        const int nf = a.park_count[0], ni = a.park_count[1];
+        const int wf = nf <= a.resume_w4 ? 4 : (nf <= a.resume_w2 ? 2 : 1);
+        const int nbf = (nf * wf + 3) / 4;   // workgroups of the finite fits
+        const int b = blockIdx.x;
+        if (b < nbf) {
+            Wr = wf;
+            const int i = b * (4 / wf) + wv / wf;
+            live = i < nf;
+            if (live) f = a.park_list[i];
+        } else {
+            if ((b - nbf) * 4 >= ni) return;   // uniform over the workgroup
+            Wr = 1;
+            const int i = (b - nbf) * 4 + wv;
+            live = i < ni;
+            if (live) f = a.park_list[a.n_fits - 1 - i];
+        }
+    } else {
+        f = blockIdx.x * (4 / W) + wv / W;   // (never a resume: that is W = 0)
+        live = f < a.n_fits;
+    }
     nm_batch_offsets(a);
     const int m = a.m;
     const int nfc = a.nj * a.R;
     double *sD2 = sm;
     double *sK = sD2 + m * m;                           // [16][IMG]
-    const int tid = threadIdx.x, wv = tid / 64;
     const int g = (tid & 63) / 16, l = tid % 16;
-    const int fs = wv / W;                              // this wave's fit within the workgroup
-    const int slot = (wv % W) * 4 + g;                  // this row's candidate slot
-    int f = blockIdx.x * FPW + fs;
+    const int fs = wv / Wr;                             // this wave's fit within the workgroup
+    const int slot = (wv % Wr) * 4 + g;                 // this row's candidate slot
+    NMCand2 *sCf = sC + 4 * Wr * fs;
     for (int i = tid; i < m * m; i += blockDim.x) sD2[i] = a.D2[i];
-    bool live = true;
-    if (a.resume) {
-        if (f >= *a.park_count) live = false;
-        else f = a.park_list[f];
-    } else if (f >= a.n_fits) {
-        live = false;
-    }
     const int fc = live ? f : 0;
     int coord, jidx;
     if (a.coord) {
@@ -1244,22 +1290,36 @@ __global__ void __launch_bounds__(256) nm_spec2_kernel(NMArgs a) {
         St.xbx = St.xby = St.xrx = St.xry = St.fxr = 0.0;
         nm_start(St, cfg, t0x, t0y);
     }
-    // workgroup-uniform rounds (a finished fit's rows evaluate a dummy point until all are done)
+    // workgroup-uniform rounds (a finished fit's rows evaluate a dummy point until all are done);
+    // with one wave per fit (Wr == 1, uniform over the workgroup: the resume's one-wave fits) each
+    // wave runs its own rounds and exchanges its candidates within the wave only
     const int lane = tid & 63;
-    while (__syncthreads_or(St.st != ST_DONE)) {
+    __syncthreads();   // sD2
+    for (;;) {
+        if (Wr == 1) {
+            if (St.st == ST_DONE) break;
+        } else if (!__syncthreads_or(St.st != ST_DONE)) {
+            break;
+        }
         const bool run = St.st != ST_DONE;   // uniform over the fit's waves
-        const NMCand2 mine = run ? nm_candidate_slot<W>(St, slot) : NMCand2{-1.0, -1.0, 0.0, -1};
+        const NMCand2 mine = run ? nm_candidate_slot(St, cfg, slot, Wr) : NMCand2{-1.0, -1.0, 0.0, -1};
         // unused slots evaluate the request itself (a duplicate; never matched)
         const double fv = gp_nlml<MAXM>(m, l, P, sD2, mine.st >= 0 ? mine.x : St.px,
                                         mine.st >= 0 ? mine.y : St.py, jit, y, Kimg);
-        if (l == 0) sC[fs][slot] = NMCand2{mine.x, mine.y, fv, mine.st};
-        __syncthreads();
+        if (l == 0) sCf[slot] = NMCand2{mine.x, mine.y, fv, mine.st};
+        if (Wr == 1) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+            __syncthreads();
+        }
         // consume every answered request in scipy's order: lane k < 4W holds candidate k; the
         // lowest matching slot answers (the order a sequential scan would take)
-        const NMCand2 ck = sC[fs][lane < 4 * W ? lane : 0];
+        const NMCand2 ck = sCf[lane < 4 * Wr ? lane : 0];
         uint64_t used = 0;
         while (run && St.st != ST_DONE) {
-            const bool match = lane < 4 * W && !((used >> lane) & 1) && ck.st == St.st && ck.x == St.px &&
+            const bool match = lane < 4 * Wr && !((used >> lane) & 1) && ck.st == St.st && ck.x == St.px &&
                                ck.y == St.py;
             const uint64_t mk = __builtin_amdgcn_ballot_w64(match);
             if (!mk) break;
@@ -1268,7 +1328,7 @@ __global__ void __launch_bounds__(256) nm_spec2_kernel(NMArgs a) {
             nm_consume(St, cfg, wave_lane_double(ck.f, hit));
         }
     }
-    if (live && (tid & (64 * W - 1)) == 0) {
+    if (live && (tid & (64 * Wr - 1)) == 0) {
         const double fval = (St.f1 != St.f1 || St.f2 != St.f2) ? NAN : St.f0;
         if (a.theta_out) { a.theta_out[2 * f] = St.s0x; a.theta_out[2 * f + 1] = St.s0y; }
         if (a.fval_out) a.fval_out[f] = fval;
@@ -1705,10 +1765,44 @@ static int spec_waves(int total, int maxm, bool resume) {
     return total <= ncu ? 4 : (total <= 2 * ncu ? 2 : 1);
 }
 
+// Finite parked-fit counts up to which the resume gives each finite fit 4 / 2 waves of the
+// two-level kernel (NNGP_RESUME_W4 / NNGP_RESUME_W2; both 0 = the one-level kernel, one wave per
+// fit, as NNGP_NM_LEVEL2=0)
+static void resume_bounds(int maxm, int &t4, int &t2) {
+    t4 = t2 = 0;
+    if (maxm > 32 || env_int("NNGP_NM_LEVEL2", 1) == 0) return;
+    static int ncu = 0;
+    if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) ncu = 256;
+    if (ncu <= 0) ncu = 256;
+    t4 = std::max(0, env_int("NNGP_RESUME_W4", ncu));
+    t2 = std::max(t4, env_int("NNGP_RESUME_W2", 2 * ncu));
+}
+
 static int run_nm_spec(NMArgs &a, hipStream_t st, int nq = 1) {
     const int maxm = maxm_for(a.m);
     const int threads = wg_threads(maxm);
     const size_t lds = sizeof(double) * ((size_t)a.m * a.m + (size_t)(threads / 16) * k_image_doubles(maxm));
+    if (a.resume && nq == 1) {
+        // the parked fits: their counts are only known on the device, so the grid covers the
+        // largest case -- finite fits on 4 waves each (<= t4 of them), 2 (<= t2) or 1, then the
+        // all-+inf fits a wave each -- and the workgroups past the counts exit at once
+        int t4, t2;
+        resume_bounds(maxm, t4, t2);
+        if (t2 > 0) {
+            a.resume_w4 = t4;
+            a.resume_w2 = t2;
+            const int q4 = (a.n_fits + 3) / 4;
+            const dim3 grid2(std::max(std::min(t4, a.n_fits), std::max((std::min(t2, a.n_fits) + 1) / 2, q4)) + q4);
+            return with_maxm(a.m, [&](auto mc) {
+                constexpr int M = decltype(mc)::value;
+                if constexpr (M <= 32) {
+                    hipLaunchKernelGGL((nm_spec2_kernel<M, 0>), grid2, dim3(256), lds, st, a);
+                    NNGP_LAUNCH_CHECK();
+                }
+                return NNGP_OK;
+            });
+        }
+    }
     const int W = spec_waves(a.n_fits * nq, maxm, a.resume != 0);
     if (W > 1) {
         const dim3 grid2((a.n_fits + 4 / W - 1) / (4 / W), nq);
@@ -1819,11 +1913,11 @@ static int run_nm_parked(NMArgs a, hipStream_t st) {
     const int cap = nm_park_cap();
     if (cap <= 0) return run_nm(a, false, st);
     int err = 0;
-    char *ws = (char *)workspace(sizeof(NM) * (size_t)a.n_fits + sizeof(int32_t) * ((size_t)a.n_fits + 1), &err, 5);
+    char *ws = (char *)workspace(sizeof(NM) * (size_t)a.n_fits + sizeof(int32_t) * ((size_t)a.n_fits + 2), &err, 5);
     if (err) return err;
     NM *park = (NM *)ws;
-    int32_t *cnt = (int32_t *)(park + a.n_fits);
-    NNGP_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int32_t), st));
+    int32_t *cnt = (int32_t *)(park + a.n_fits);   // [finite parked, all-+inf parked], list
+    NNGP_HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(int32_t), st));
     a.park_cap = cap;
     // jitter-major rows (NNGP_NM_JMAJOR=0: product order): fits sharing a jitter run similar
     // evaluation counts, so a wave's rows finish together (d = 800 synthetic correction
@@ -1831,7 +1925,7 @@ static int run_nm_parked(NMArgs a, hipStream_t st) {
     a.jmajor = env_int("NNGP_NM_JMAJOR", 1);
     a.park = park;
     a.park_count = cnt;
-    a.park_list = cnt + 1;
+    a.park_list = cnt + 2;
     int rc = run_nm(a, false, st);
     if (rc) return rc;
     a.park_cap = 0;

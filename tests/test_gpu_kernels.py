@@ -382,6 +382,43 @@ def test_fhn_pde_full_size_vs_oracle(gpu, nx, n_slices, norm):
         assert np.array_equal(out[i], so.rk(8, T[i], T[i + 1], 6, U0[i], O.STEP_FIXED)), i
 
 
+@pytest.mark.parametrize('d,w4,w2,n400', [(150, None, None, 250), (150, '0', '0', 250), (150, '0', '100000', 250),
+                                         (150, '100000', '100000', 250), (20, None, None, 40), (50, None, None, 90)])
+def test_predict_parked_all_inf_fits_vs_oracle(gpu, d, w4, w2, n400, monkeypatch):
+    """Exactly duplicated training rows make K + jitter*I singular in floating point for the jitters
+    <= 1e-16 (1 + j == 1): those fits' simplices are all +inf and run to maxfev = 400, like the
+    parked tail of a real FHN-PDE d = 800 correction.
+    - d = 150, m = 20 (1 350 fits, the packed kernel): fits still running at 70 evaluations are
+      parked, the finite ones at the front of the park list and the all-+inf ones at its back.
+      The resume gives a finite fit 4 waves of the two-level kernel (default: up to #CU of them;
+      NNGP_RESUME_W4/W2 = 100000 forces it), 2 (W4 = 0, W2 = 100000) or 1 (both 0: the one-level
+      kernel), and an all-+inf fit one wave.
+    - d = 20 / 50 (180 / 450 fits: the two-level kernel from the start, 4 / 2 waves per fit): an
+      all-+inf simplex takes W whole iterations per round -- each wave answers the requests the
+      state machine makes if the earlier ones are +inf too.
+    Every case is bitwise the oracle."""
+    import torch
+    for k, v in (('NNGP_RESUME_W4', w4), ('NNGP_RESUME_W2', w2)):
+        if v is not None:
+            monkeypatch.setenv(k, v)
+    m = 20
+    rng = np.random.default_rng(150)
+    base = np.cumsum(0.005 * rng.standard_normal((40, d)), axis=0)
+    X = np.repeat(base, 4, axis=0)          # every state 4 times: duplicated kernel rows
+    Y = np.sin(3 * X) + 1e-5 * rng.standard_normal(X.shape)
+    q = X[30] + 0.01
+    mdl = gpu.NNGP_p(n=d, N=4, nn=m, n_restarts=1, seed=9)
+    th0 = mdl.draw_thetas(1)
+    fits = torch.empty((mdl.n_fits, 4), dtype=torch.float64, device='cuda')
+    preds = mdl.predict_device(_t(torch, X), _t(torch, Y), X.shape[0], _t(torch, q), _t(torch, th0),
+                               fits_out=fits).cpu().numpy()
+    ora, ofits = O.predict(X, Y, q, m, th0, return_fits=True)
+    f = fits.cpu().numpy()
+    assert (f[:, 3] >= 400).sum() >= n400   # fits that ran to maxfev (d = 150: 304 of 1 350; 716 parked)
+    assert np.array_equal(f, ofits)
+    assert np.array_equal(preds, ora)
+
+
 def test_predict_fhn_pde_d800_vs_oracle(gpu):
     """BASELINE configs[4]'s correction shape: FHN-PDE d = 800, m = 20, R = 1 (FHN_PDE.py:175-176):
     7 200 fits per prediction -- the packed fits kernel with the tail hand-off (fits still running

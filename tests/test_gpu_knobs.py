@@ -38,7 +38,8 @@ KNOBS = [
     ('burgers', 'NNGP_NM_PARK', '0'), ('burgers', 'NNGP_CHAIN', '1'), ('fhn512', 'NNGP_D2_WAVES', '0'),
     ('fhn512', 'NNGP_FHN_PAIR', '0'), ('fhn512', 'NNGP_NM_PARK', '0'), ('fhn512', 'NNGP_NM_PARK', '20'),
     ('fhn512', 'NNGP_RK_THREADS', '512'), ('lorenz', 'NNGP_RK_GROUP', '0'), ('lorenz', 'NNGP_CHAIN', '1'),
-    ('lorenz', 'NNGP_NM_LEVEL2', '0'),
+    ('lorenz', 'NNGP_NM_LEVEL2', '0'), ('fhn512', 'NNGP_RESUME_W4', '0'), ('fhn512', 'NNGP_RESUME_W4', '100000'),
+    ('fhn512', 'NNGP_RESUME_W2', '0'),
 ]
 
 
