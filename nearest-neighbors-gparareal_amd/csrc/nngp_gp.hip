@@ -1753,7 +1753,7 @@ static int run_mean(NMArgs &a, hipStream_t st) {
 // workgroup for m > 32)
 // waves per fit of the two-level kernel for a launch of `total` fits: 4 while every fit's four
 // waves get a SIMD of their own (total <= #CU), 2 up to twice that, else the one-level kernel.
-// Resumed (parked) fits keep one wave each: their count is only known on the device.
+// (Resumed parked fits take their shape on the device instead: run_nm_spec / resume_bounds.)
 // NNGP_NM_LEVEL2=0 disables it.
 static int spec_waves(int total, int maxm, bool resume) {
     const int e = env_int("NNGP_NM_LEVEL2", 1);
