@@ -221,10 +221,18 @@ int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mode
  * misses finished by the host's fits.  Returns launches; *slices_out (HOST, optional). */
 int64_t nngp_chain_stats(int64_t *slices_out);
 
+/* Sweeps (this process) that were run a second time with the speculative batch serialised
+ * because a hit slice's wait for the overlapped batch timed out (NNGP_SPEC_WAIT_US, default 2 s;
+ * the first pass wrote nothing for that slice, and the rerun gives the same bits).            */
+int64_t nngp_sweep_late_reruns(void);
+
 /* Drains the device and releases every resource the library holds (workspaces, side streams,
  * events, host-mapped flags); the next call re-creates what it needs.  Registered with atexit
  * by the Python package, so none of them is left to the HIP runtime's process-exit teardown.
- * (No reference counterpart: the reference holds no device resources.)  Returns 0. */
+ * (No reference counterpart: the reference holds no device resources.)  Returns 0.
+ * Threading: the library serves one host thread per process (the reference's host loop is
+ * single-threaded, parareal.py); nngp_shutdown must not run while another thread is inside a
+ * library call. */
 int nngp_shutdown(void);
 
 /* ---- 4. full-data GParareal (models.GPjax_p, models.py:273-473) ------------------------------

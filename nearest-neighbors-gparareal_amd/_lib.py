@@ -23,7 +23,7 @@ STEP_FIXED, STEP_LINSPACE, STEP_CONTRACT = 0, 1, 16
 EXPORTS = ['nngp_abi_version', 'nngp_last_error', 'nngp_device_count', 'nngp_rk_batch', 'nngp_rk_batch_grid',
            'nngp_rhs_batch', 'nngp_parareal_update', 'nngp_knn', 'nngp_nm_fit_batch',
            'nngp_gp_mean', 'nngp_predict', 'nngp_correction_sweep', 'nngp_gpfull_lml', 'nngp_gpfull_fit',
-           'nngp_gpfull_mean', 'nngp_predict_range', 'nngp_chain_stats', 'nngp_shutdown']
+           'nngp_gpfull_mean', 'nngp_predict_range', 'nngp_chain_stats', 'nngp_sweep_late_reruns', 'nngp_shutdown']
 MODEL_PARAREAL, MODEL_NNGP, MODEL_GPFULL = 0, 1, 2
 
 
@@ -81,10 +81,13 @@ def lib():
     L.nngp_gpfull_mean.argtypes = [_vp, i64, i32, _vp, _vp, _vp, _vp, _vp, _vp]
     L.nngp_chain_stats.argtypes = [ctypes.POINTER(i64)]
     L.nngp_chain_stats.restype = i64
+    L.nngp_sweep_late_reruns.argtypes = []
+    L.nngp_sweep_late_reruns.restype = i64
     L.nngp_predict_range.argtypes = [_vp, _vp, i64, i32, _vp, i32, i32, _dp, i32, _vp, i32, i32, dbl, dbl, i32,
                                      _vp, _vp]
     for name in EXPORTS:
-        if name not in ('nngp_abi_version', 'nngp_last_error', 'nngp_device_count', 'nngp_chain_stats'):
+        if name not in ('nngp_abi_version', 'nngp_last_error', 'nngp_device_count', 'nngp_chain_stats',
+                        'nngp_sweep_late_reruns'):
             getattr(L, name).restype = i32
     if L.nngp_abi_version() != 1:
         raise NNGPError('ABI version mismatch')
@@ -136,3 +139,9 @@ def chain_stats():
     sl = ctypes.c_int64(0)
     n = L.nngp_chain_stats(ctypes.byref(sl))
     return int(n), int(sl.value)
+
+
+def sweep_late_reruns():
+    """Sweeps rerun with the speculative batch serialised after a hit's wait timed out
+    (include/nngp.h nngp_sweep_late_reruns), in this process."""
+    return int(lib().nngp_sweep_late_reruns())

@@ -18,6 +18,11 @@ inline int env_int(const char *name, int dflt) {
     return e ? atoi(e) : dflt;
 }
 
+// attributes of the CURRENT device (hipGetDevice), cached per device: compute units, and the
+// rate of the 100 MHz wall clock the kernels read (wall_clock64) in kHz
+int device_cus();
+double device_wallclock_khz();
+
 // thread-local last error, returned by nngp_last_error()
 void set_error(const char *fmt, ...);
 

@@ -785,11 +785,14 @@ struct NMArgs {
     int32_t *park_list, *park_count;
     // overlapped speculative batch: the fits kernel counts each prediction's finished fits
     // (done[blockIdx.y], after a device-scope fence); the sweep's mean kernel, on a hit served by
-    // that batch, waits until wait_done reaches wait_n (bounded: *err = 1 past ~2 s)
+    // that batch, waits until wait_done reaches wait_n -- for at most wait_ticks of the 100 MHz
+    // wall clock (NNGP_SPEC_WAIT_US, default 2 s; 0 = give up at once); past that, or once an
+    // earlier slice has given up (*err != 0), it sets *err and writes nothing
     int32_t *done;
     const int32_t *wait_done;
     int wait_n;
     int32_t *err;
+    uint64_t wait_ticks;
 };
 
 // apply the blockIdx.y prediction offsets of a batched launch (all zero otherwise)
@@ -1360,14 +1363,18 @@ __device__ __forceinline__ void gp_mean_dev(const NMArgs &a, int blk, bool load_
         if (tid == 0) {
             s_late = 0;
             if (__hip_atomic_load(a.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
-                uint32_t spin = 0;
+                // never a hang: past the deadline flag it and write nothing; the host redoes the
+                // sweep without the overlap.  Once any slice has given up, later slices do not
+                // wait at all (the rerun recomputes them).
+                const uint64_t t0 = wall_clock64();
                 while (__hip_atomic_load(a.wait_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.wait_n) {
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++spin > (1u << 24)) {   // never a hang: flag it, write nothing; the host
-                        s_late = 1;              // redoes the sweep without the overlap
+                    if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
+                        wall_clock64() - t0 >= a.wait_ticks) {
+                        s_late = 1;
                         __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                         break;
                     }
+                    __builtin_amdgcn_s_sleep(2);
                 }
                 __threadfence();
             }
@@ -1475,23 +1482,39 @@ struct ChainArgs {
     int32_t *stop;             // host-mapped: the slice the chain stopped at (a miss), or N
     uint64_t *g_ticks;         // host-mapped: wall-clock ticks spent in G
     uint64_t *prof;            // host-mapped [4] or null (NNGP_CHAIN_PROF): ticks in G | kNN | select | mean
+    int32_t *berr;             // host-mapped: a grid barrier timed out (every workgroup then leaves)
+    uint64_t bar_ticks;        // that timeout, in wall-clock ticks (2 s)
 };
 
 // all workgroups of the (co-resident) grid: arrivals counted on one agent-scope
 // counter; the fences make every workgroup's global writes before the barrier visible to every
-// workgroup after it (L2 write-back / invalidate across the XCDs)
-__device__ __forceinline__ void chain_barrier(uint32_t *bar, uint32_t &target) {
+// workgroup after it (L2 write-back / invalidate across the XCDs).  Bounded: a workgroup that waits
+// longer than bar_ticks (the grid was not co-resident after all -- e.g. another process's kernels
+// hold CUs), or that sees another workgroup's timeout, flags *berr and returns false; the kernel
+// then ends and the host reruns the sweep on the launch chain (nngp_sweep.hip).
+__device__ __forceinline__ bool chain_barrier(uint32_t *bar, uint32_t &target, int32_t *berr, uint64_t ticks) {
+    __shared__ int s_bad;
     __syncthreads();
-    if (gridDim.x == 1) return;
+    if (gridDim.x == 1) return true;
     target += gridDim.x;
     if (threadIdx.x == 0) {
+        s_bad = 0;
         __threadfence();
         __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target)
+        const uint64_t t0 = wall_clock64();
+        while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (__hip_atomic_load(berr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
+                wall_clock64() - t0 >= ticks) {
+                __hip_atomic_store(berr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                s_bad = 1;
+                break;
+            }
             __builtin_amdgcn_s_sleep(1);
+        }
         __threadfence();
     }
     __syncthreads();
+    return s_bad == 0;
 }
 
 template <int SYS, int ORDER>
@@ -1617,7 +1640,7 @@ __global__ void __launch_bounds__(256) chain_kernel(ChainArgs c) {
         // 2) distances of every training row (grid-stride over the workgroups)
         for (int64_t r = (int64_t)blockIdx.x * 256 + tid; r < c.rows; r += (int64_t)gridDim.x * 256)
             c.dist[r] = knn_dist_row(c.X, d, qs, r);
-        chain_barrier(c.bar, target);
+        if (!chain_barrier(c.bar, target, c.berr, c.bar_ticks)) break;
         CHAIN_MARK(1);
         // 3) ordered neighbour list, y_m, D2, kd2 and the hit code
         if (blockIdx.x == 0) {
@@ -1645,7 +1668,7 @@ __global__ void __launch_bounds__(256) chain_kernel(ChainArgs c) {
             }
         }
         if (prof && tid == 0) cyc += clock64();
-        chain_barrier(c.bar, target);
+        if (!chain_barrier(c.bar, target, c.berr, c.bar_ticks)) break;
         CHAIN_MARK(2);
         const int hit = __hip_atomic_load(c.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (hit == 0) break;   // uniform over the grid: the host runs this slice's fits
@@ -1662,7 +1685,7 @@ __global__ void __launch_bounds__(256) chain_kernel(ChainArgs c) {
             gp_mean_dev<MAXM>(a, blk, first);
             first = false;
         }
-        chain_barrier(c.bar, target);
+        if (!chain_barrier(c.bar, target, c.berr, c.bar_ticks)) break;
         CHAIN_MARK(3);
     }
 #undef CHAIN_MARK
@@ -1759,9 +1782,7 @@ static int spec_waves(int total, int maxm, bool resume) {
     const int e = env_int("NNGP_NM_LEVEL2", 1);
     if (maxm > 32 || resume || e == 0) return 1;
     if (e == 2 || e == 4) return e;   // forced (measurements)
-    static int ncu = 0;
-    if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) ncu = 256;
-    if (ncu <= 0) ncu = 256;
+    const int ncu = device_cus();
     return total <= ncu ? 4 : (total <= 2 * ncu ? 2 : 1);
 }
 
@@ -1771,9 +1792,7 @@ static int spec_waves(int total, int maxm, bool resume) {
 static void resume_bounds(int maxm, int &t4, int &t2) {
     t4 = t2 = 0;
     if (maxm > 32 || env_int("NNGP_NM_LEVEL2", 1) == 0) return;
-    static int ncu = 0;
-    if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) ncu = 256;
-    if (ncu <= 0) ncu = 256;
+    const int ncu = device_cus();
     t4 = std::max(0, env_int("NNGP_RESUME_W4", ncu));
     t2 = std::max(t4, env_int("NNGP_RESUME_W2", 2 * ncu));
 }
@@ -1833,9 +1852,7 @@ static int run_nm_spec(NMArgs &a, hipStream_t st, int nq = 1) {
 static bool use_spec(int n_fits, int m) {
     const int forced = env_int("NNGP_NM_SPEC", -1);
     if (forced >= 0) return forced != 0;
-    static int ncu = 0;
-    if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) ncu = 256;
-    if (ncu <= 0) ncu = 256;
+    const int ncu = device_cus();
     const int mm = maxm_for(m);   // m > 32: one fit per 64-thread workgroup, ~1 workgroup per CU (LDS)
     return n_fits <= (mm <= 16 ? 8 : (mm <= 32 ? 4 : 1)) * ncu;
 }
@@ -1860,9 +1877,7 @@ static int run_nm(NMArgs &a, bool fused, hipStream_t st, int nq = 1, int qslot =
         // whole coordinates per workgroup (the arg-min needs all fits of a coordinate); few per
         // workgroup so the latency-bound fits spread over every CU, capped by LDS / threads
         const int nfc = a.nj * a.R;
-        static int ncu = 0;
-        if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) ncu = 256;
-        if (ncu <= 0) ncu = 256;
+        const int ncu = device_cus();
         auto thr = [&](int c) { return ((c * nfc * 16 + 63) / 64) * 64; };
         int cpw = std::max(1, std::min((a.d + ncu - 1) / ncu, a.d));
         while (cpw > 1 && (lds_of(thr(cpw)) > 150 * 1024 || thr(cpw) > tmax)) cpw--;
@@ -2078,6 +2093,8 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
             a.wait_done = wait_done;
             a.wait_n = (int)n_fits;
             a.err = wait_err;
+            const double us = std::max(0, env_int("NNGP_SPEC_WAIT_US", 2000000));
+            a.wait_ticks = (uint64_t)(us * device_wallclock_khz() / 1e3);
         }
     }
     if (use_spec(a.n_fits, a.m)) {   // fits (a wave each), then arg-min + mean (+ bias) per coordinate
@@ -2220,8 +2237,7 @@ bool chain_supported(const nngp_system *sys, int g_step_mode, int m) {
 // teardown at process exit crashed under rocprofv3: profiles/r03/chain_exit_crash.txt.)
 template <int MAXM>
 static int chain_launch(ChainArgs &c, int nb, size_t lds, hipStream_t st) {
-    static int ncu = 0;
-    if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) ncu = 0;
+    const int ncu = device_cus();
     int per_cu = 0;
     NNGP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<MAXM>, 256, lds));
     NNGP_REQUIRE(per_cu >= 1 && (int64_t)per_cu * ncu >= nb, "chain: %d workgroups cannot be co-resident", nb);
@@ -2294,6 +2310,8 @@ int chain_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t 
     c.g_ticks = (uint64_t *)(res->stop + 2);
     const bool prof = env_int("NNGP_CHAIN_PROF", 0) != 0;
     c.prof = prof ? (uint64_t *)(res->stop + 4) : nullptr;
+    c.berr = res->stop + 28;   // byte 112 of the 128-byte host-mapped block (prof: bytes 16..87)
+    c.bar_ticks = (uint64_t)(2.0e6 * res->tick_khz / 1e3);   // 2 s
     const int maxm = maxm_for(m);
     const size_t lds = std::max(knn_xs_bytes(m, d),
                                 sizeof(double) * ((size_t)m * m + m + 16 * k_image_doubles(maxm)));
@@ -2302,6 +2320,7 @@ int chain_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t 
     // barrier, measured slower: 65 us per slice, 0.387 s for Burgers N=128)
     const int nb = std::max(1, std::min(c.n_mean_blk, 64));
     res->stop[0] = -1;
+    __atomic_store_n(c.berr, 0, __ATOMIC_RELEASE);
     NNGP_HIP_CHECK(hipMemsetAsync(res->bar, 0, sizeof(uint32_t), st));
     switch (maxm) {
     case 8: rc = chain_launch<8>(c, nb, lds, st); break;
@@ -2313,6 +2332,11 @@ int chain_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t 
     }
     if (rc) return rc;
     NNGP_HIP_CHECK(hipStreamSynchronize(st));
+    if (__atomic_load_n(c.berr, __ATOMIC_ACQUIRE) != 0) {   // not co-resident: the caller reruns
+        set_error("chain: a grid barrier timed out (NNGP_CHAIN=1 needs the device to itself)");
+        *stop_out = -2;
+        return NNGP_E_HIP;
+    }
     const int stop = __atomic_load_n(res->stop, __ATOMIC_ACQUIRE);
     if (stop < i0 || stop > N) {
         set_error("chain: the kernel reported no stop slice (%d)", stop);

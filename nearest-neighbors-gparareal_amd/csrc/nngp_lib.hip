@@ -53,6 +53,41 @@ void *workspace(size_t bytes, int *err, int slot) {
     return w.ptr;
 }
 
+static std::mutex g_attr_mu;
+static std::vector<int> g_cus;
+static std::vector<double> g_khz;
+
+static void device_attrs(int *cus, double *khz) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    std::lock_guard<std::mutex> lk(g_attr_mu);
+    if ((int)g_cus.size() <= dev) {
+        g_cus.resize(dev + 1, 0);
+        g_khz.resize(dev + 1, 0.0);
+    }
+    if (g_cus[dev] <= 0) {
+        int n = 0, k = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        if (hipDeviceGetAttribute(&k, hipDeviceAttributeWallClockRate, dev) != hipSuccess || k <= 0) k = 100000;
+        g_cus[dev] = n;
+        g_khz[dev] = k;
+    }
+    if (cus) *cus = g_cus[dev];
+    if (khz) *khz = g_khz[dev];
+}
+
+int device_cus() {
+    int n;
+    device_attrs(&n, nullptr);
+    return n;
+}
+
+double device_wallclock_khz() {
+    double k;
+    device_attrs(nullptr, &k);
+    return k;
+}
+
 // nngp_shutdown: free every workspace slot (re-allocated on next use)
 static void ws_release() {
     std::lock_guard<std::mutex> lk(g_ws_mu);

@@ -201,7 +201,11 @@ __device__ __forceinline__ void nn_sincos(double x, double &sn, double &cs) {
 // odd polynomial r + r^3 P(r^2) (8 coefficients, a weighted minimax fit of sin(r)/r - 1 on
 // [0, (pi/2)^2] computed with mpmath, relative error 2.8e-19; tests/golden/sin_pi_fit.py) and the
 // sign (-1)^n as a sign-bit xor.  No quadrant select between two polynomials, so ~20 VALU
-// instead of ~40 per sine.  <= 2 ulp from glibc (tests/test_oracle_golden.py).
+// instead of ~40 per sine.  <= 2 ulp from glibc (tests/test_oracle_golden.py: |x| <= 40 and the
+// field's whole attractor range |x| <= b/a = 20 with margin, 2e5 points on |x| <= 25; |x| <= 1e4).
+// Range of validity: the parity trick needs |n| < 2^51, i.e. |x| < pi*2^51; the three-term
+// reduction keeps the 2-ulp bound only while n*PI_3's rounding stays far below r's ulp (measured
+// to |x| = 1e4; ThomasLabyrinth's states stay within |x| <= 20).
 struct SinPiC {
     static constexpr double INVPI = 0x1.45f306dc9c883p-2;
     static constexpr double PI_1 = 2 * 1.57079632673412561417e+00, PI_2 = 2 * 6.07710050630396597660e-11,

@@ -9,6 +9,7 @@
 // Python costs tens of microseconds of interpreter/ctypes work per launch; here the loop issues the
 // launches back to back on one stream, so the GPU never waits for the host.
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -136,6 +137,9 @@ static int respec_window() {
 // Speculation policy: worth it while the batch of every slice's fits is a throughput-shaped
 // launch much cheaper than the latency-bound sweep it shortens (Burgers N=128: 146k fits; not
 // FHN-PDE d=800 N=512: 3.7M).  NNGP_SPEC_MAX_FITS overrides the bound (0 disables).
+// sweeps rerun with the batch serialised because a hit's wait timed out (nngp_sweep_late_reruns)
+static std::atomic<int64_t> g_late_reruns{0};
+
 static bool speculate_ok(int speculate, int64_t nq, int64_t n_fits) {
     if (speculate == 0 || nq < 2) return false;
     if (speculate > 0) return true;
@@ -149,7 +153,8 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
                             const double *UG, int model, const double *X, const double *Y, int64_t rows, int m,
                             int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
                             double fatol, double xatol, int maxfev, double *preds_scratch, int speculate,
-                            int32_t *spec_hits_out, float *g_ms_out, void *stream, bool allow_overlap, int *late) {
+                            int32_t *spec_hits_out, float *g_ms_out, void *stream, bool allow_overlap,
+                            bool allow_chain, int *late) {
     using namespace nngp;
     *late = 0;
     NNGP_REQUIRE(sys != nullptr && t && U1 && UG1, "null argument");
@@ -194,7 +199,7 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
     // overlapped batch (NNGP_SPEC_OVERLAP, default 1; launch chain only): the batch's fits run on a
     // side stream while the sweep starts as soon as the batch's neighbour lists exist; a hit slice's
     // mean waits for that slice's fits only (per-prediction completion counters)
-    const bool chained = spec && chain_supported(sys, g_step_mode, m);
+    const bool chained = spec && allow_chain && chain_supported(sys, g_step_mode, m);
     const bool overlap = spec && !chained && allow_overlap && env_int("NNGP_SPEC_OVERLAP", 1) != 0;
     int32_t *done = nullptr;
     if (spec) {
@@ -260,6 +265,7 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
             rc = chain_sweep(sys, g_tableau, g_step_mode, g_steps, t, I, N, i, U1, UG1, X, Y, rows, m, n_jitter,
                              jitter_exp_host, n_restarts, flags, spec_idx, spec_fits, W > 0 ? spec2_idx : nullptr,
                              W > 0 ? spec2_fits : nullptr, preds_scratch, &s, &g_ms, st);
+            if (rc && s == -2) *late = 1;   // a grid barrier timed out: rerun on the launch chain
             if (rc || s >= N) break;
             // miss at slice s: G(U1[s]) and its select are done (the chain kernel has drained)
             const size_t j = (size_t)(s - I);
@@ -325,6 +331,8 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
         if (rc || W == 0 || i + 1 >= N) continue;
         int32_t hit = 0;
         rc = wait_flag(rs->hflags + j, st, &hit);
+        // a mean that gave up waiting for the overlapped batch: stop issuing, the caller reruns
+        if (rc == NNGP_OK && overlap && __atomic_load_n(rs->herr, __ATOMIC_ACQUIRE) != 0) break;
         if (rc || hit != 0) continue;
         // miss: re-guess slices i+1 .. i+w from the actual U1[i] on the side stream
         const int w = (int)std::min<int64_t>(W, N - 1 - i);
@@ -393,15 +401,20 @@ extern "C" int nngp_correction_sweep(const nngp_system *sys, int g_tableau, int 
                                      double *preds_scratch, int speculate, int32_t *spec_hits_out,
                                      float *g_ms_out, void *stream) {
     // The sweep writes UG1[i+1] and U1[i+1] for i >= I only and reads none of them before writing,
-    // so a sweep whose overlapped batch fell behind (see correction_sweep) is simply run again
-    // with the batch serialised: the same bits, later.
+    // so a sweep whose overlapped batch fell behind, or whose fused chain's grid barrier timed out
+    // (see correction_sweep), is simply run again with the batch serialised on the launch chain:
+    // the same bits, later.
     int late = 0;
     int rc = correction_sweep(sys, g_tableau, g_step_mode, g_steps, t, I, N, U1, UG1, UF, UG, model, X, Y, rows, m,
                               n_jitter, jitter_exp_host, n_restarts, theta0, fatol, xatol, maxfev, preds_scratch,
-                              speculate, spec_hits_out, g_ms_out, stream, true, &late);
-    if (rc != NNGP_OK && late)
+                              speculate, spec_hits_out, g_ms_out, stream, true, true, &late);
+    if (rc != NNGP_OK && late) {
+        g_late_reruns.fetch_add(1);
         rc = correction_sweep(sys, g_tableau, g_step_mode, g_steps, t, I, N, U1, UG1, UF, UG, model, X, Y, rows, m,
                               n_jitter, jitter_exp_host, n_restarts, theta0, fatol, xatol, maxfev, preds_scratch,
-                              speculate, spec_hits_out, g_ms_out, stream, false, &late);
+                              speculate, spec_hits_out, g_ms_out, stream, false, false, &late);
+    }
     return rc;
 }
+
+extern "C" int64_t nngp_sweep_late_reruns(void) { return g_late_reruns.load(); }

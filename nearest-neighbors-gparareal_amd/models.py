@@ -172,11 +172,23 @@ class NNGP_p(ModelAbstr):
 
     def _host(self):
         if self._host_xy is None:
+            if self._dev_xy is None:
+                raise AttributeError("'NNGP_p' has no training set yet: call fit(x, y, k) first")
             self._host_xy = tuple(v.detach().cpu().numpy() for v in self._dev_xy)
         return self._host_xy
 
-    x = property(lambda self: self._host()[0])
-    y = property(lambda self: self._host()[1])
+    def _set_xy(self, i, v):
+        """Reference-style assignment `mdl.x = ...` / `mdl.y = ...` (plain attributes there,
+        models.py:157-159): the host pair is updated and the device copy dropped, so the next
+        prediction uploads the assigned set."""
+        pair = list(self._host_xy) if self._host_xy is not None else (
+            [v_.detach().cpu().numpy() for v_ in self._dev_xy] if self._dev_xy is not None else [None, None])
+        pair[i] = v
+        self._host_xy = tuple(pair)
+        self._dev_xy = None
+
+    x = property(lambda self: self._host()[0], lambda self, v: self._set_xy(0, v))
+    y = property(lambda self: self._host()[1], lambda self, v: self._set_xy(1, v))
 
     # ---------------------------------------------------------------------------- device path
     def predict_device(self, X, Y, rows, new_x, theta0, out=None, bias=None, preds=None,
@@ -202,7 +214,9 @@ class NNGP_p(ModelAbstr):
     def predict(self, new_x, prev_F=None, prev_G=None, *args, **kwargs):
         """models.py:171-183 (host arrays in/out; kNN + fits + argmin + mean on the GPU)."""
         torch = _lib.require_gpu()
-        if self._dev_xy is None:   # fit() was given host arrays
+        if self._dev_xy is None:   # fit() was given host arrays (or x / y were assigned)
+            if self._host_xy is None or self._host_xy[0] is None or self._host_xy[1] is None:
+                raise AttributeError("'NNGP_p' has no training set yet: call fit(x, y, k) first")
             self._dev_xy = (_lib.as_device(self._host_xy[0]), _lib.as_device(self._host_xy[1]))
         X, Y = self._dev_xy
         q = torch.tensor(np.asarray(new_x, dtype=np.float64).reshape(-1), device='cuda')

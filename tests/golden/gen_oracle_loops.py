@@ -10,6 +10,8 @@ here; the oracle is pinned to it by tests/test_oracle_golden.py.
     python tests/golden/gen_oracle_loops.py fhn800_n512_nngp       # ~15 min
     python tests/golden/gen_oracle_loops.py burgers_pub_nngp_s45_sumorder   # K's roundoff sensitivity
     python tests/golden/gen_oracle_loops.py tomlab256_nngp         # TomLab N=256 to convergence
+    python tests/golden/gen_oracle_loops.py burgers128_seeds       # BASELINE configs[2], seeds 0-7 + serial fine
+    python tests/golden/gen_oracle_loops.py fhn800_fine            # configs[4]'s serial fine solution (~1e8 steps)
 """
 import hashlib
 import os
@@ -83,6 +85,61 @@ def tomlab256():
     return o, time.time() - t0
 
 
+def burgers_fine(so, u0, N=128, Nf=2000, tspan=(0, 5)):
+    """The serial fine solution at the slice boundaries (slice by slice, the F propagator of every
+    slice applied to the previous slice's end state -- what a converged Parareal run must equal to
+    the convergence tolerance): [N+1][d]."""
+    t = np.linspace(tspan[0], tspan[1], N + 1)
+    fine = [np.asarray(u0, dtype=float)]
+    for i in range(N):
+        fine.append(so.rk(8, t[i], t[i + 1], Nf, fine[-1]))
+    return np.array(fine)
+
+
+def burgers128_seeds(seeds):
+    """BASELINE configs[2] (Burgers_perf_across_m.py:30-33: d = 128, N = 128, T = 5, F = RK8 2 000 /
+    G = RK1 4 steps per slice, '-11' with bounds [0, 1], nn = 15) for several seeds: K, conv_int, a
+    digest of every iterate, and the serial fine solution at the slice boundaries with each seed's
+    final-state error against it."""
+    so = O.System('burgers', d=128, param=(0.01,), mn=0.0, mx=1.0)
+    x = np.linspace(-1, 1, 128)
+    u0 = so.fit(0.5 * (np.cos(4.5 * np.pi * x) + 1))
+    fine = burgers_fine(so, u0)
+    out = {'seeds': np.array(seeds), 'fine': fine}
+    ks, convs, digs, errs, secs = [], [], [], [], []
+    for sd in seeds:
+        t0 = time.time()
+        o = O.parareal(so, [0, 5], 128, 4, 2000, 'RK1', 'RK8', epsilon=5e-7, model='nngp', nn=15, seed=sd, u0=u0)
+        ks.append(o['k'])
+        convs.append(np.array(o['conv_int'] + [-1] * (128 - len(o['conv_int']))))
+        digs.append(u_digest(o['u']))
+        errs.append(np.max(np.abs(o['u'][:, :, -1] - fine)))
+        secs.append(time.time() - t0)
+        print(f'burgers128 seed {sd}: K={o["k"]} conv_int={o["conv_int"]} final err {errs[-1]:.3e} '
+              f'({secs[-1]:.0f} s)', flush=True)
+    out.update(k=np.array(ks), conv_int=np.array(convs), digest=np.array(digs),
+               final_err=np.array(errs), seconds=np.array(secs))
+    return out
+
+
+def fhn800_fine(rows):
+    """The serial fine solution of BASELINE configs[4] (fhn800 above) at the slice boundaries
+    `rows`: 512 slices x 195 325 RK8 steps one after another (about 1e8 steps, single thread)."""
+    so = O.System('fhn_pde', nx=20, normalized=False)
+    np.random.seed(45)
+    u = np.random.Generator(np.random.get_bit_generator()).uniform(size=800)
+    t = np.linspace(0, 1100, 513)
+    keep = {0: u.copy()}
+    t0 = time.time()
+    for i in range(512):
+        u = so.rk(8, t[i], t[i + 1], 195325, u)
+        if i + 1 in rows:
+            keep[i + 1] = u.copy()
+        if i % 16 == 15:
+            print(f'fhn800 fine: slice {i + 1}/512 ({time.time() - t0:.0f} s)', flush=True)
+    return np.array([keep[r] for r in rows]), time.time() - t0
+
+
 def main(which):
     if which.startswith('burgers_pub') and 'sumorder' in which:
         # roundoff sensitivity of K on the published schedule: the same run with the GP solves and
@@ -107,6 +164,17 @@ def main(which):
         rows = np.array([0, 1, 2, 3, 128, 256, 384, 510, 511, 512])
         np.savez_compressed(os.path.join(HERE, f'{which}.npz'), k=o['k'], conv_int=np.array(o['conv_int']),
                             rows=rows, u_rows=o['u'][rows], digest=u_digest(o['u']), seconds=sec)
+    elif which == 'burgers128_seeds':
+        out = burgers128_seeds(list(range(8)))
+        np.savez_compressed(os.path.join(HERE, f'{which}.npz'), **out)
+        print(which, 'K', out['k'].tolist(), 'final err', out['final_err'].tolist(), flush=True)
+        return
+    elif which == 'fhn800_fine':
+        rows = np.load(os.path.join(HERE, 'fhn800_n512_nngp.npz'))['rows']
+        fine, sec = fhn800_fine(set(int(r) for r in rows))
+        np.savez_compressed(os.path.join(HERE, f'{which}.npz'), rows=rows, fine_rows=fine, seconds=sec)
+        print(which, f'{sec:.0f} s', flush=True)
+        return
     else:
         raise SystemExit(f'unknown case {which}')
     print(which, 'K', o['k'], 'conv_int', o['conv_int'], 'converged', o['converged'], f'{sec:.0f} s', flush=True)

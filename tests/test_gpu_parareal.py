@@ -90,18 +90,6 @@ def test_fhn_ode_matches_reference(gpu):
     assert set(r['timings']) >= {'F_time', 'G_time', 'mdl_tot_t', 'runtime', 'F_time_serial_avg'}
 
 
-@pytest.mark.slow
-@pytest.mark.parametrize('seed', [0, 1, 2])
-def test_burgers_n128_k_in_published_distribution(gpu, seed):
-    """BASELINE configs[2]: Burgers d=128, N=128, T=5, F=RK8 2000/slice, G=RK1 4/slice, m=15
-    (Burgers_perf_across_m.py:30-33): the reference's 100 seeds gave K in {9: 68, 10: 32}."""
-    ode = gpu.Burgers(d_x=128, normalization='-11')
-    s = gpu.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
-    p = gpu.Parareal(ode, s, [0, 5], 128, epsilon=5e-7, verbose=None)
-    r = p.run(model='nngp', nn=15, seed=seed)
-    assert r['converged'] and r['k'] in (9, 10)
-
-
 def test_tomlab_nngp_bitwise_equals_oracle_loop(gpu):
     """ThomasLabyrinth (TomLab.py settings: RK4/RK1, m=18, fatol=xatol=1e-3) on a short span: the
     sin-based field and the m=18 fits (24-row padded kernel) match the oracle's loop bit for bit."""
@@ -307,3 +295,24 @@ def test_fused_chain_is_bitwise_the_launch_chain(gpu, case, monkeypatch):
     assert np.array_equal(np.nan_to_num(a['u'], nan=7.0), np.nan_to_num(b['u'], nan=7.0))
     assert n1 > n0 and s1 - s0 == sum(b['timings']['spec_hits'])
     assert b['timings']['G_time'] > 0
+
+
+def test_late_overlapped_batch_rerun_is_bitwise(gpu, monkeypatch):
+    """The overlapped speculative batch's recovery path: with NNGP_SPEC_WAIT_US=0 a hit slice whose
+    batch fits are not finished gives up at once, writes nothing, later hit slices stop waiting,
+    and nngp_correction_sweep reruns the sweep with the batch serialised.  The run must be bitwise
+    the default one, and the rerun must really have happened."""
+    from nngp_amd import _lib
+    ode = gpu.Burgers(d_x=128, normalization='-11')
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
+    kw = dict(model='nngp', nn=15, seed=45, early_stop=3, speculate=1)
+    a = gpu.Parareal(ode, s, [0, 5], 128, epsilon=5e-7, verbose=None).run(**kw)
+    n0 = _lib.sweep_late_reruns()
+    monkeypatch.setenv('NNGP_SPEC_WAIT_US', '0')
+    b = gpu.Parareal(ode, s, [0, 5], 128, epsilon=5e-7, verbose=None).run(**kw)
+    late = _lib.sweep_late_reruns() - n0
+    print('late reruns', late, 'hits', b['timings']['spec_hits'])
+    assert late >= 1
+    assert a['k'] == b['k'] and a['conv_int'] == b['conv_int']
+    assert a['timings']['spec_hits'] == b['timings']['spec_hits']
+    assert np.array_equal(np.nan_to_num(a['u'], nan=7.0), np.nan_to_num(b['u'], nan=7.0))

@@ -70,6 +70,18 @@ def test_burgers_published_schedule_nngp_s45_bitwise_oracle_loop(gpu):
     assert r['converged'] == bool(P['converged'])
     assert np.array_equal(np.nan_to_num(r['u'][:, :, -1], nan=7.0), np.nan_to_num(P['u_last'], nan=7.0))
     assert u_digest(r['u']) == str(P['digest'])
+    # Against the published run itself: its per-iteration maxima over the slices of
+    # err = ||u^{k+1} - u^k||_inf (new_lib.py:1038), as VERDICT.md (round 3) quotes them from
+    # Burges_scal_final_5_128_nngp (this repo's permitted safe loaders refuse that pickle, DESIGN.md
+    # §5).  Iterations 1-7 agree in magnitude (a factor of 2); the published run's iteration-8
+    # maximum 7.37e-7 sits above epsilon = 5e-7 and ours below it, which is why the published
+    # run needed a 9th iteration and this one stops at K = 8: a threshold straddle.
+    published = [0.117, 0.0179, 3.03e-3, 4.99e-4, 4.62e-5, 4.13e-6, 2.39e-6, 7.37e-7, 2.87e-7]
+    ours = [float(np.nanmax(r['err'][:, k])) for k in range(r['k'])]
+    print('per-iteration max err: ours', [f'{v:.3g}' for v in ours], 'published', published)
+    for k in range(7):
+        assert 0.5 <= ours[k] / published[k] <= 2.0, (k + 1, ours[k], published[k])
+    assert r['k'] == 8 and ours[7] < 5e-7 < published[7]
 
 
 @pytest.mark.skipif(os.environ.get('NNGP_PUBLISHED') != '1', reason='set NNGP_PUBLISHED=1 (K spread over seeds)')
@@ -94,6 +106,9 @@ def test_fhn_pde_d512_published_k(gpu):
     print(f"FHN-PDE d=512 N=512: K={r['k']} (published 6) conv_int={r['conv_int']} "
           f"runtime={r['timings']['runtime']:.1f}s")
     assert r['converged'] and r['k'] == 6
+    # the published run's converged-interval sequence (FHN_scal_times_16_512_nngp, as VERDICT.md
+    # round 3 quotes it; the pickle itself is refused by the permitted safe loaders)
+    assert r['conv_int'] == [1, 2, 3, 4, 7, 512]
 
 
 def fhn800_n512(gpu, ng=50, nf=195325):

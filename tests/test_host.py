@@ -224,3 +224,43 @@ def test_adaptive_nn_warns_up_front_when_n_could_outgrow_the_fits(monkeypatch):
         warnings.simplefilter('always')
         p.run(model='nngp', nn='adaptive', early_stop=40)
     assert not any('adaptive' in str(x.message) for x in w)
+
+
+@pytest.mark.parametrize('n', [1, 2])
+def test_bench_gpus_flag_launches_that_many_ranks(n):
+    """`bench.py --gpus N` run bare (no WORLD_SIZE) starts N ranks itself (torch.distributed.run as a
+    child process) and its line reports the world the process group saw; --dry-run does the same
+    launch on gloo without a GPU.  A world that does not match --gpus exits non-zero."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK')}
+    p = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--gpus', str(n), '--dry-run'],
+                       capture_output=True, text=True, timeout=240, env=env, cwd='/tmp')
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert rec['n_gpus'] == n and rec['ranks_seen'] == list(range(n)) and rec['dry_run']
+    # a launcher world that disagrees with --gpus is refused
+    bad = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--gpus', str(n + 1), '--dry-run'],
+                         capture_output=True, text=True, timeout=240, cwd='/tmp',
+                         env=dict(env, WORLD_SIZE='1', RANK='0', LOCAL_RANK='0'))
+    assert bad.returncode != 0 and 'process group has 1 ranks' in bad.stderr
+
+
+def test_nngp_training_set_attributes_behave_like_the_reference():
+    """NNGP_p.x / .y are plain attributes in the reference (models.py:157-159): readable after
+    fit, assignable (the next prediction uses the assigned set), and a clear AttributeError
+    before any training set exists."""
+    import nngp_amd
+    m = nngp_amd.NNGP_p(n=3, N=8, nn=10)
+    with pytest.raises(AttributeError, match='fit'):
+        m.x
+    m.fit(np.zeros((4, 3)), np.ones((4, 3)), k=0)
+    assert m.x.shape == (4, 3) and np.all(m.y == 1)
+    m.x = np.full((5, 3), 2.0)
+    m.y = np.full((5, 3), 3.0)
+    assert np.all(m.x == 2) and np.all(m.y == 3) and m._dev_xy is None

@@ -105,8 +105,9 @@ def test_math_accuracy():
         assert np.max(np.abs(got - r) / np.maximum(np.spacing(np.abs(r)), np.spacing(1.0) * 2 ** -10)) <= 2, fn
     assert np.isnan(L.nn_sin(np.inf)) and np.isnan(L.nn_cos(np.nan))
     assert np.isnan(L.nn_sin_pi(np.inf)) and np.isnan(L.nn_sin_pi(-np.inf)) and np.isnan(L.nn_sin_pi(np.nan))
-    # the pi-reduced sine at 200k points of ThomasLabyrinth's range (|x| <= 15) and at +-0
-    xs = rng.uniform(-15, 15, 200000)
+    # the pi-reduced sine at 200k points covering ThomasLabyrinth's attractor bound |x| <= b/a = 20
+    # (systems.py:257-271, a = 0.5, b = 10) with margin, and at +-0
+    xs = np.concatenate([rng.uniform(-25, 25, 200000), [20.0, -20.0, 25.0, -25.0]])
     got = np.array([L.nn_sin_pi(x) for x in xs])
     assert np.max(np.abs(got - np.sin(xs)) / np.maximum(np.spacing(np.abs(np.sin(xs))), 2.0 ** -1074)) <= 2
     assert L.nn_sin_pi(0.0) == 0.0 and L.nn_sin_pi(1e-300) == 1e-300   # (the sign of a zero is not kept)
