@@ -264,6 +264,42 @@ int nngp_gpfull_fit(const double *X, int64_t rows, int d, const double *Y, int n
 int nngp_gpfull_mean(const double *X, int64_t rows, int d, const double *q, const double *coef,
                      const double *alpha, const double *bias, double *out, void *stream);
 
+/* ---- 5. multi-GPU: one RCCL communicator per process (one process per GPU) -------------------
+ * Replaces the reference's task farm across MPI ranks (parareal.py:310-315, F over slices;
+ * models.py:197-202, fits over the pool; launched as `srun ... mpi4py.futures`, Hopf.py:43-46) with
+ * the two exchanges of SURVEY.md §8e.  RCCL is resolved at run time (the process's loaded
+ * librccl.so.1 -- torch's -- else the system's), so the library loads without it; every call
+ * below returns NNGP_E_UNSUPPORTED when it is absent.
+ * nngp_comm_unique_id: rank 0 creates the id (NNGP_COMM_UID_BYTES bytes, HOST), the caller
+ *   broadcasts it (e.g. torch.distributed.broadcast_object_list); nngp_comm_init: every rank, on
+ *   its device (collective); nngp_comm_size: (ranks, rank) of the live communicator, (0, -1) if
+ *   none; nngp_comm_destroy: releases it (nngp_shutdown does too).                              */
+#define NNGP_COMM_UID_BYTES 128
+int nngp_comm_unique_id(void *uid_out);
+int nngp_comm_init(int nranks, int rank, const void *uid);
+int nngp_comm_size(int *nranks_out, int *rank_out);
+int nngp_comm_destroy(void);
+
+/* All-gather of equal [per_rank_elems] fp64 blocks in rank order, recv = [nranks][per_rank_elems]
+ * (DEVICE; send may be recv + rank*per_rank_elems, in place): the ONE collective of a Parareal
+ * iteration -- the fine end states of every rank's contiguous slice block (parareal.py:310-315's
+ * gather), stream-ordered on `stream`.                                                          */
+int nngp_allgather_states(const double *send, double *recv, size_t per_rank_elems, void *stream);
+
+/* nngp_correction_sweep for NNGP_MODEL_NNGP with every prediction's d*n_jitter*n_restarts fits
+ * sharded by coordinate over the communicator's ranks (rank r fits coordinates
+ * [r*chunk, min((r+1)*chunk, d)), chunk = ceil(d/nranks)): per slice G (replicated), this rank's
+ * coordinates (nngp_predict_range), one in-place all-gather of the predictions, and
+ * U1[i+1] = preds + UG1[i+1] -- all on `stream`, no host synchronisation.  Bitwise the unsharded
+ * sweep on every rank (same inputs, same theta0 draws).  gather: DEVICE [nranks*chunk] scratch.
+ * No speculation (every rank would need the whole batch).                                       */
+int nngp_correction_sweep_sharded(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps,
+                                  const double *t, int I, int N, double *U1, double *UG1, const double *X,
+                                  const double *Y, int64_t rows, int m, int n_jitter,
+                                  const double *jitter_exp_host, int n_restarts, const double *theta0,
+                                  double fatol, double xatol, int maxfev, double *gather, float *g_ms_out,
+                                  void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,7 +23,9 @@ STEP_FIXED, STEP_LINSPACE, STEP_CONTRACT = 0, 1, 16
 EXPORTS = ['nngp_abi_version', 'nngp_last_error', 'nngp_device_count', 'nngp_rk_batch', 'nngp_rk_batch_grid',
            'nngp_rhs_batch', 'nngp_parareal_update', 'nngp_knn', 'nngp_nm_fit_batch',
            'nngp_gp_mean', 'nngp_predict', 'nngp_correction_sweep', 'nngp_gpfull_lml', 'nngp_gpfull_fit',
-           'nngp_gpfull_mean', 'nngp_predict_range', 'nngp_chain_stats', 'nngp_sweep_late_reruns', 'nngp_shutdown']
+           'nngp_gpfull_mean', 'nngp_predict_range', 'nngp_chain_stats', 'nngp_sweep_late_reruns', 'nngp_shutdown',
+           'nngp_comm_unique_id', 'nngp_comm_init', 'nngp_comm_size', 'nngp_comm_destroy', 'nngp_allgather_states',
+           'nngp_correction_sweep_sharded']
 MODEL_PARAREAL, MODEL_NNGP, MODEL_GPFULL = 0, 1, 2
 
 
@@ -83,6 +85,14 @@ def lib():
     L.nngp_chain_stats.restype = i64
     L.nngp_sweep_late_reruns.argtypes = []
     L.nngp_sweep_late_reruns.restype = i64
+    L.nngp_comm_unique_id.argtypes = [ctypes.c_char_p]
+    L.nngp_comm_init.argtypes = [i32, i32, ctypes.c_char_p]
+    L.nngp_comm_size.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    L.nngp_comm_destroy.argtypes = []
+    L.nngp_allgather_states.argtypes = [_vp, _vp, ctypes.c_size_t, _vp]
+    L.nngp_correction_sweep_sharded.argtypes = [ctypes.POINTER(CSystem), i32, i32, i64, _vp, i32, i32, _vp, _vp,
+                                                _vp, _vp, i64, i32, i32, _dp, i32, _vp, dbl, dbl, i32, _vp,
+                                                ctypes.POINTER(ctypes.c_float), _vp]
     L.nngp_predict_range.argtypes = [_vp, _vp, i64, i32, _vp, i32, i32, _dp, i32, _vp, i32, i32, dbl, dbl, i32,
                                      _vp, _vp]
     for name in EXPORTS:
@@ -145,3 +155,36 @@ def sweep_late_reruns():
     """Sweeps rerun with the speculative batch serialised after a hit's wait timed out
     (include/nngp.h nngp_sweep_late_reruns), in this process."""
     return int(lib().nngp_sweep_late_reruns())
+
+
+COMM_UID_BYTES = 128
+_comm_key = None
+
+
+def comm_for(group=None):
+    """The library's RCCL communicator (include/nngp.h nngp_comm_*) over the torch.distributed
+    `group`, created once per group: rank 0 makes the unique id, torch broadcasts it, every rank
+    joins on its current device.  Returns True when the native collectives are live for `group`;
+    False for a gloo group (ranks sharing one GPU: RCCL refuses duplicate devices) or when RCCL
+    cannot be loaded -- the caller then keeps torch.distributed's collectives."""
+    global _comm_key
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_backend(group) != 'nccl':
+        return False
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    key = (id(group), world, rank)
+    if _comm_key == key:
+        return True
+    L = lib()
+    uid = ctypes.create_string_buffer(COMM_UID_BYTES)
+    ok = [True]
+    if rank == 0:
+        ok[0] = L.nngp_comm_unique_id(uid) == 0
+    obj = [(ok[0], uid.raw)]
+    src = 0 if group is None else dist.get_global_rank(group, 0)
+    dist.broadcast_object_list(obj, src=src, group=group)
+    if not obj[0][0]:
+        return False
+    check(L.nngp_comm_init(world, rank, obj[0][1]))
+    _comm_key = key
+    return True

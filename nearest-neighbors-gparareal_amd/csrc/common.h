@@ -60,9 +60,10 @@ void set_error(const char *fmt, ...);
 // speculative sweep's batch buffers, which must outlive the per-slice calls.  Growing a slot
 // frees the old buffer after hipFree's implicit device synchronisation.  Not thread-safe across
 // host threads sharing a device.
-constexpr int N_WS_SLOTS = 9;   // slot 2: the sweep's speculation buffers; 3: full-GP factors; 4: fit queues; 5: parked fits;
+constexpr int N_WS_SLOTS = 10;   // slot 2: the sweep's speculation buffers; 3: full-GP factors; 4: fit queues; 5: parked fits;
                                 // 6: the re-speculation window's batch (slot 1 may still be read by an overlapped batch);
-                                // 7 / 8: the fit queues of the overlapped batch / of the re-speculation window
+                                // 7 / 8: the fit queues of the overlapped batch / of the re-speculation window;
+                                // 9: the sharded sweep's zeros (nngp_comm.hip)
 void *workspace(size_t bytes, int *err, int slot = 0);
 
 int predict_impl(const double *X, const double *Y, int64_t rows, int d, const double *new_x, int m,
@@ -79,8 +80,11 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
                double fatol, double xatol, int maxfev, int32_t *idx_out, double *fits_out, bool latency,
                hipStream_t st, int slot = 1, int32_t *done = nullptr, hipEvent_t ev_select = nullptr);
 // the fused correction chain (nngp_gp.hip): one persistent kernel per run of hit slices
-void chain_release();   // nngp_shutdown's parts (nngp_gp.hip / nngp_sweep.hip)
+void chain_release();   // nngp_shutdown's parts (nngp_gp.hip / nngp_sweep.hip / nngp_comm.hip)
 void sweep_release();
+void comm_release();
+// grow-only pool of timing events (nngp_sweep.hip): *out = n events
+int timing_events(size_t n, hipEvent_t **out);
 bool chain_supported(const nngp_system *sys, int g_step_mode, int m);
 int chain_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps, const double *t, int I,
                 int N, int i0, double *U1, double *UG1, const double *X, const double *Y, int64_t rows, int m,

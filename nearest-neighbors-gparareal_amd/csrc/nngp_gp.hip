@@ -786,8 +786,8 @@ struct NMArgs {
     // overlapped speculative batch: the fits kernel counts each prediction's finished fits
     // (done[blockIdx.y], after a device-scope fence); the sweep's mean kernel, on a hit served by
     // that batch, waits until wait_done reaches wait_n -- for at most wait_ticks of the 100 MHz
-    // wall clock (NNGP_SPEC_WAIT_US, default 2 s; 0 = give up at once); past that, or once an
-    // earlier slice has given up (*err != 0), it sets *err and writes nothing
+    // wall clock (NNGP_SPEC_WAIT_US, default 2 s; 0 = give up at once, even if the fits are done);
+    // past that, or once an earlier slice has given up (*err != 0), it sets *err and writes nothing
     int32_t *done;
     const int32_t *wait_done;
     int wait_n;
@@ -1366,9 +1366,12 @@ __device__ __forceinline__ void gp_mean_dev(const NMArgs &a, int blk, bool load_
                 // never a hang: past the deadline flag it and write nothing; the host redoes the
                 // sweep without the overlap.  Once any slice has given up, later slices do not
                 // wait at all (the rerun recomputes them).
+                // wait_ticks == 0 (NNGP_SPEC_WAIT_US=0): give up at once, fits finished or not --
+                // the deterministic way into the rerun path (tests)
                 const uint64_t t0 = wall_clock64();
-                while (__hip_atomic_load(a.wait_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.wait_n) {
-                    if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
+                while (a.wait_ticks == 0 ||
+                       __hip_atomic_load(a.wait_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.wait_n) {
+                    if (a.wait_ticks == 0 || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
                         wall_clock64() - t0 >= a.wait_ticks) {
                         s_late = 1;
                         __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

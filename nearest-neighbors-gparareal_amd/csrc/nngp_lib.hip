@@ -108,6 +108,7 @@ extern "C" int nngp_shutdown(void) {
     (void)hipDeviceSynchronize();
     nngp::chain_release();
     nngp::sweep_release();
+    nngp::comm_release();
     nngp::ws_release();
     return NNGP_OK;
 }

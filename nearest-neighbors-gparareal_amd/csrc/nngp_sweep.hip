@@ -20,7 +20,7 @@ namespace nngp {
 static std::vector<hipEvent_t> g_events;
 static std::mutex g_events_mu;
 
-static int timing_events(size_t n, hipEvent_t **out) {
+int timing_events(size_t n, hipEvent_t **out) {
     std::lock_guard<std::mutex> lk(g_events_mu);
     while (g_events.size() < n) {
         hipEvent_t e;

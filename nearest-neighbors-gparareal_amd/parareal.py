@@ -66,6 +66,8 @@ class _Events:
 
     def collect(self):
         out = {}
+        if self.pairs:
+            self.pairs[-1][1].synchronize()   # stream-ordered: the last event completes last
         for a, b, k in self.pairs:
             out[k] = out.get(k, 0.0) + a.elapsed_time(b) / 1e3
         self.pairs = []
@@ -114,14 +116,24 @@ def fine_sweep_sharded(propagate, t, U, UF, I, N, group=None):
     rank = dist.get_rank(group)
     lo, hi, chunk = shard_bounds(I, N, world, rank)
     n = U.shape[1]
-    send = torch.zeros((chunk, n), dtype=U.dtype, device=U.device)
-    if hi > lo:
-        propagate(t[lo:hi], t[lo + 1:hi + 1], U[lo:hi].contiguous(), send[:hi - lo])
     if dist.get_backend(group) == 'gloo':
+        send = torch.zeros((chunk, n), dtype=U.dtype, device=U.device)
+        if hi > lo:
+            propagate(t[lo:hi], t[lo + 1:hi + 1], U[lo:hi].contiguous(), send[:hi - lo])
         gathered = _gloo_all_gather(send, group, world)
     else:
-        gathered = torch.empty((world * chunk, n), dtype=U.dtype, device=U.device)
-        dist.all_gather_into_tensor(gathered, send, group=group)
+        # RCCL over xGMI: each rank integrates straight into its block of the gather buffer, then
+        # ONE in-place all-gather -- the library's communicator (nngp_allgather_states) when live,
+        # torch.distributed's otherwise
+        gathered = torch.zeros((world * chunk, n), dtype=U.dtype, device=U.device)
+        send = gathered[rank * chunk:(rank + 1) * chunk]
+        if hi > lo:
+            propagate(t[lo:hi], t[lo + 1:hi + 1], U[lo:hi].contiguous(), send[:hi - lo])
+        if _lib.comm_for(group):
+            _lib.check(_lib.lib().nngp_allgather_states(send.data_ptr(), gathered.data_ptr(), chunk * n,
+                                                        torch.cuda.current_stream().cuda_stream))
+        else:
+            dist.all_gather_into_tensor(gathered, send, group=group)
     UF[I + 1:N + 1] = gathered[:N - I]
 
 
@@ -419,27 +431,45 @@ class Parareal():
 
     def _shard_corrections(self, model):
         """Shard each prediction's fits by coordinate over the process group: Parareal(...,
-        shard_corrections=True/False) or run(..., shard_corrections=...) for one run; default when
-        more than one rank and d*9*R >= 2048."""
+        shard_corrections=True/False) or run(..., shard_corrections=...) for one run (True applies
+        at any world size, one rank included); by default when more than one rank and
+        d*9*R >= 2048."""
         import torch
         dist = torch.distributed
-        if self.process_group is None and not (dist.is_available() and dist.is_initialized()):
-            return False
-        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(self.process_group) == 1:
+        if not (dist.is_available() and dist.is_initialized()):
             return False
         shard = getattr(self, '_run_shard', self.shard_corrections)
         if shard is not None:
             return bool(shard)
-        return model.n_fits >= 2048
+        return dist.get_world_size(self.process_group) > 1 and model.n_fits >= 2048
 
     def _correction_sweep_sharded(self, torch, model, t_dev, I, N, U1, UG1, X, Y, rows, th0, stream):
-        """correction_sweep_sharded with the HIP launches: G via the solver, nngp_predict_range
-        for this rank's coordinates, u = (preds - 0) + uG via nngp_parareal_update (bitwise the
-        fused kernel's mean + uG)."""
+        """correction_sweep_sharded with the HIP launches.  On an NCCL group with the library's
+        communicator live (and native_comm, default True): ONE native call,
+        nngp_correction_sweep_sharded, that issues every slice's G, this rank's coordinates, the
+        RCCL all-gather of the predictions and u = preds + uG on the stream with no host round trip.
+        Otherwise (gloo: ranks sharing one GPU) the same launches from Python: G via the solver,
+        nngp_predict_range for this rank's coordinates, u = (preds - 0) + uG via
+        nngp_parareal_update (bitwise the fused kernel's mean + uG)."""
         lib, solver, n = _lib.lib(), self.solver, self.n
         m = min(model.n_neighbours(), int(rows))
         jit, jp = _lib.host_doubles(JITTERS)
         nf = model.n_fits
+        if getattr(self, '_run_native_comm', True) and _lib.comm_for(self.process_group) and \
+                not solver.coarse_is_paged():
+            world = torch.distributed.get_world_size(self.process_group)
+            chunk = (n + world - 1) // world
+            gather = torch.zeros(world * chunk, dtype=torch.float64, device=U1.device)
+            cs = solver.f.csystem(U1.device)
+            g_ms = ctypes.c_float(0.0)
+            _lib.check(lib.nngp_correction_sweep_sharded(
+                ctypes.byref(cs), _lib.TABLEAU[solver.G], solver.step_mode, solver.Ng, t_dev.data_ptr(), I, N,
+                U1.data_ptr(), UG1.data_ptr(), X.data_ptr(), Y.data_ptr(), int(rows), m, len(jit), jp,
+                model.n_restarts, th0.data_ptr(), float(model.fatol), float(model.xatol), model.maxfev,
+                gather.data_ptr(), ctypes.byref(g_ms), stream))
+            model.train_count += nf * (N - I)
+            self.spec_hits.append(0)
+            return g_ms.value / 1e3
         zeros = torch.zeros(n, dtype=torch.float64, device=U1.device)
         ev = _Events(torch)
 
@@ -537,6 +567,7 @@ class Parareal():
         # run(..., speculate=, shard_corrections=) override the constructor's settings for this run
         self._run_speculate = int(kwargs.get('speculate', self.speculate))
         self._run_shard = kwargs.get('shard_corrections', self.shard_corrections)
+        self._run_native_comm = bool(kwargs.get('native_comm', True))
         tspan, N, epsilon, n = self.tspan, self.N, self.epsilon, self.n
         solver = self.solver
         verbose = kwargs.get('verbose', self.verbose)

@@ -51,3 +51,54 @@ def test_multi_rank_gpu_run_equals_single_rank(gpu, case, shard, world, tmp_path
     R = np.load(out)
     assert int(R['k']) == k1 and list(R['conv']) == list(conv1)
     assert np.array_equal(np.nan_to_num(R['u'], nan=7.0), np.nan_to_num(u1, nan=7.0))
+
+
+@pytest.mark.timeout(300)
+def test_native_rccl_comm_and_sharded_sweep_one_rank(gpu, tmp_path):
+    """The C-ABI's multi-GPU exchange on the box's one GPU: an NCCL (RCCL) process group of one
+    rank, the library's communicator created from it (_lib.comm_for), nngp_allgather_states, and
+    nngp_correction_sweep_sharded (every slice's G, this rank's coordinates, the RCCL all-gather and
+    u = preds + uG issued natively) -- bitwise the unsharded run, with and without the native path.
+    Several ranks need several GPUs for RCCL (the 8-GPU bench runs them); the orchestration across
+    ranks is covered on gloo above."""
+    out = str(tmp_path / 'comm.npz')
+    code = r'''
+import os, sys, socket
+import numpy as np
+import torch
+sys.path.insert(0, os.environ["NNGP_ROOT"]); sys.path.insert(0, os.path.join(os.environ["NNGP_ROOT"], "tests"))
+torch.cuda.set_device(0)
+with socket.socket() as s:
+    s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]
+torch.distributed.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                     device_id=torch.device("cuda", 0))
+import nngp_amd as g
+from nngp_amd import _lib
+from dist_gpu_worker import run_case
+assert _lib.comm_for(None)
+L = _lib.lib()
+import ctypes
+nr, rk = ctypes.c_int(0), ctypes.c_int(0)
+L.nngp_comm_size(ctypes.byref(nr), ctypes.byref(rk))
+assert (nr.value, rk.value) == (1, 0)
+x = torch.arange(10, dtype=torch.float64, device="cuda"); y = torch.zeros(10, dtype=torch.float64, device="cuda")
+_lib.check(L.nngp_allgather_states(x.data_ptr(), y.data_ptr(), 10, torch.cuda.current_stream().cuda_stream))
+torch.cuda.synchronize(); assert torch.equal(x, y)
+k0, c0, u0 = run_case(g, "fhn", None)          # unsharded (world 1)
+k1, c1, u1 = run_case(g, "fhn", True)          # native sharded sweep
+ode = g.FHN_PDE(d_x=10)
+s = g.SolverRK(ode.get_vector_field(), Ng=5, Nf=100, F="RK8", G="RK4")
+r2 = g.Parareal(ode, s, [0, 8], 16, epsilon=5e-7, verbose=None).run(model="nngp", nn=20, seed=45, early_stop=2,
+                                                                  shard_corrections=True, native_comm=False)
+np.savez(sys.argv[1], k=[k0, k1, r2["k"]], same_native=np.array_equal(np.nan_to_num(u0, nan=7.0), np.nan_to_num(u1, nan=7.0)),
+         same_py=np.array_equal(np.nan_to_num(u0, nan=7.0), np.nan_to_num(r2["u"], nan=7.0)),
+         conv=[list(c0) == list(c1), list(c0) == list(r2["conv_int"])])
+torch.distributed.destroy_process_group()
+print("comm ok")
+'''
+    root = os.path.dirname(HERE)
+    p = subprocess.run([sys.executable, '-c', code, out], env=dict(os.environ, NNGP_ROOT=root),
+                       capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+    R = np.load(out)
+    assert len(set(R['k'].tolist())) == 1 and bool(R['same_native']) and bool(R['same_py']) and all(R['conv'])
