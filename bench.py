@@ -116,6 +116,10 @@ def fine_sweep_bench(torch, g, world, rank, steps, warmup, steps_per_slice, slic
     out = torch.empty_like(u0)
     gathered = torch.empty((n_total, 3), dtype=torch.float64, device='cuda')
     ev = []
+    # the all-gather of the end states: the library's RCCL communicator (include/nngp.h
+    # nngp_allgather_states), torch.distributed's if it cannot be created
+    native = world > 1 and g._lib.comm_for(None)
+    st = torch.cuda.current_stream().cuda_stream
 
     def one(record):
         if record:
@@ -126,7 +130,9 @@ def fine_sweep_bench(torch, g, world, rank, steps, warmup, steps_per_slice, slic
         if record:
             b.record()
             ev.append((a, b))
-        if world > 1:
+        if native:
+            g._lib.check(g.lib().nngp_allgather_states(out.data_ptr(), gathered.data_ptr(), out.numel(), st))
+        elif world > 1:
             torch.distributed.all_gather_into_tensor(gathered, out)
 
     for _ in range(warmup):
@@ -142,7 +148,8 @@ def fine_sweep_bench(torch, g, world, rank, steps, warmup, steps_per_slice, slic
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(tt.item())
     kernel_s = np.mean([a.elapsed_time(b) / 1e3 for a, b in ev])
-    return elapsed, kernel_s, n_total, out
+    return elapsed, kernel_s, n_total, out, ('nngp_allgather_states' if native else
+                                             ('torch all_gather_into_tensor' if world > 1 else None))
 
 
 def corrections_bench(torch, g, m=15, R=2, n_slices=128):
@@ -648,12 +655,14 @@ def fhn_strong(torch, g, world, rank, steps=3, warmup=1, sample=400, n_pred=4):
 
     corrections()
     c_s = timed(corrections, 1) / n_pred
+    sweep_res = sharded_sweep_timing(torch, g, solver, td, Ufull, Xd, Yd, rows, mdl, world, rank, timed)
     res = {'workload': 'FHN-PDE d=800 (d_x=20) N=512, RK8 fine sweep + coordinate-sharded nnGP corrections (m=20)',
            'world': world, 'slices_per_rank': (n_sl + world - 1) // world,
            'F_us_per_step': f_s / sample * 1e6, 'F_steps_per_s': n_sl * sample / f_s,
            'correction_ms': c_s * 1e3, 'corrections_per_s': 1 / c_s,
            'iteration_s_projected': f_s / sample * steps_it + (n_sl - 1) * c_s,
-           'sample': f'{sample} RK8 steps x 512 slices; {n_pred} corrections of 7200 fits (rows {rows})'}
+           'sample': f'{sample} RK8 steps x 512 slices; {n_pred} corrections of 7200 fits (rows {rows})',
+           'correction_sweep': sweep_res}
     if world == 1:   # the 8-GPU per-rank shares, measured on this GPU
         sh = 64
         sweep8 = lambda: solver.run_F_batch(td[:sh], td[1:sh + 1], Ud[:sh].contiguous(), out=UF[1:sh + 1])
@@ -676,6 +685,70 @@ def fhn_strong(torch, g, world, rank, steps=3, warmup=1, sample=400, n_pred=4):
                                       'note': 'excludes the per-iteration all-gather (3.3 MB) and the '
                                               'per-slice all-gather of 800 predictions (6.4 KB)'}
     return res
+
+
+def sharded_sweep_timing(torch, g, solver, td, Ufull, Xd, Yd, rows, mdl, world, rank, timed, n_sw=8):
+    """The sequential correction sweep (parareal.py:359-382) over n_sw consecutive FHN-PDE d=800
+    slices (G = RK4 50 steps, m = 20, 7 200 fits per prediction), two ways:
+    - 'python_loop': the launches issued one by one from Python per slice -- G, this rank's
+      coordinates (nngp_predict_range), the all-gather of the predictions (torch.distributed),
+      u = preds + uG (parareal.correction_sweep_sharded's pattern);
+    - 'native': ONE library call for the whole sweep -- nngp_correction_sweep_sharded over the
+      library's RCCL communicator when the job has more than one rank, nngp_correction_sweep
+      (speculation off) on one rank.
+    The difference per slice is the host overhead the native call removes."""
+    import ctypes
+    from nngp_amd.models import JITTERS
+    from nngp_amd.parareal import shard_bounds
+    lib = g.lib()
+    d = Xd.shape[1]
+    m, nf = 20, mdl.n_fits
+    jit = np.ascontiguousarray(JITTERS)
+    jp = jit.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    th = torch.tensor(mdl.draw_thetas(n_sw), dtype=torch.float64, device='cuda')
+    cs = solver.f.csystem(Xd.device)
+    st = torch.cuda.current_stream().cuda_stream
+    U1 = Ufull.clone()
+    UG1 = torch.empty_like(U1)
+    zeros = torch.zeros(d, dtype=torch.float64, device='cuda')
+    c0, c1, chunk = shard_bounds(0, d, world, rank)
+    gather = torch.zeros(world * chunk, dtype=torch.float64, device='cuda')
+    comm = world > 1 and g._lib.comm_for(None)
+
+    def python_loop():
+        for i in range(n_sw):
+            solver.run_G_batch(td[i:i + 1], td[i + 1:i + 2], U1[i:i + 1], out=UG1[i + 1:i + 2])
+            send = gather[rank * chunk:(rank + 1) * chunk]
+            if c1 > c0:
+                g._lib.check(lib.nngp_predict_range(Xd.data_ptr(), Yd.data_ptr(), rows, d, U1[i].data_ptr(), m,
+                                                    len(jit), jp, 1, th[i * nf:(i + 1) * nf].data_ptr(), c0, c1,
+                                                    0.1, 0.1, 400, send.data_ptr(), st))
+            if world > 1:
+                torch.distributed.all_gather_into_tensor(gather, send)
+            g._lib.check(lib.nngp_parareal_update(d, gather.data_ptr(), zeros.data_ptr(), UG1[i + 1].data_ptr(),
+                                                  U1[i + 1].data_ptr(), st))
+
+    def native():
+        if comm:
+            g._lib.check(lib.nngp_correction_sweep_sharded(
+                ctypes.byref(cs), 4, 0, 50, td.data_ptr(), 0, n_sw, U1.data_ptr(), UG1.data_ptr(), Xd.data_ptr(),
+                Yd.data_ptr(), rows, m, len(jit), jp, 1, th.data_ptr(), 0.1, 0.1, 400, gather.data_ptr(), None, st))
+        else:
+            scratch = torch.empty(d, dtype=torch.float64, device='cuda')
+            g._lib.check(lib.nngp_correction_sweep(
+                ctypes.byref(cs), 4, 0, 50, td.data_ptr(), 0, n_sw, U1.data_ptr(), UG1.data_ptr(), None, None,
+                g._lib.MODEL_NNGP, Xd.data_ptr(), Yd.data_ptr(), rows, m, len(jit), jp, 1, th.data_ptr(), 0.1, 0.1,
+                400, scratch.data_ptr(), 0, None, None, st))
+
+    out = {}
+    for name, fn in (('python_loop', python_loop), ('native', native)):
+        fn()
+        out[f'{name}_ms_per_slice'] = timed(fn, 2) / n_sw * 1e3
+    out['host_overhead_ms_per_slice_removed'] = out['python_loop_ms_per_slice'] - out['native_ms_per_slice']
+    out['native_path'] = ('nngp_correction_sweep_sharded (library RCCL communicator)' if comm
+                          else 'nngp_correction_sweep (one rank)')
+    out['slices'] = n_sw
+    return out
 
 
 def read_traffic():
@@ -749,7 +822,7 @@ def main():
     import nngp_amd as g
     g.lib()
 
-    elapsed, kernel_s, n_total, _ = fine_sweep_bench(torch, g, world, rank, args.steps, args.warmup,
+    elapsed, kernel_s, n_total, _, gather_path = fine_sweep_bench(torch, g, world, rank, args.steps, args.warmup,
                                                      args.steps_per_slice, args.slices_per_gpu)
     total_steps = n_total * args.steps_per_slice * args.steps
     value = total_steps / elapsed
@@ -764,7 +837,8 @@ def main():
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
         'config': {'workload': 'nonautonomous Hopf (Hopf.py), RK4 fine sweep, 13.6e6 steps/slice',
                    'slices_per_gpu': args.slices_per_gpu, 'total_slices': n_total,
-                   'steps_per_slice': args.steps_per_slice, 'parallelism': f'time-slices x{world}'},
+                   'steps_per_slice': args.steps_per_slice, 'parallelism': f'time-slices x{world}',
+                   'allgather': gather_path},
         'roofline': {'bound': 'fp64-valu', 'achieved': achieved_tf, 'peak': FP64_PEAK_TFLOPS,
                      'unit': 'TFLOP/s', 'frac': achieved_tf / FP64_PEAK_TFLOPS, 'traffic': traffic,
                      **({k: v for k, v in tr.items() if k != 'traffic'} if tr else {}), 'traffic_source': tr_src,

@@ -423,21 +423,14 @@ __global__ void __launch_bounds__(EPT == 1 ? 1024 : (EPT == 2 ? 512 : 256)) rk_f
 // instead of the element-per-thread kernel's 2 writes + 14 reads.  Same expressions, same order
 // (systems.py:365-366) -- bitwise rk_field_kernel<FHN_PDE>.  d = 2 nx^2 <= 2048.
 //
-// LDS layout: FHN_PAIR_IMAGES images of [u | v], each field at a fixed stride of FHN_PAIR_PS
-// doubles, and a stage's image fixed at compile time (stage s of every step uses image s & 1, the
-// last of an odd stage count image 2, so the image a stage writes was last read two barriers
-// earlier).  Every LDS access of the step loop is then one of five per-thread neighbour addresses
-// plus an immediate offset: no address arithmetic per stage (round 2 recomputed buf * d + c_i
-// for all ten reads and two writes of every stage, ~11 of its ~70 VALU).  Threads past the grid
-// (the last wave's idle lanes) compute point 0's stencil on their own zeros and write their
-// garbage to the images' padding, so the step loop has no branch either.
+// LDS layout: FhnPairImages::N images of [point][u, v] (below), and a stage's image fixed at
+// compile time (stage s of every step uses image s & 1, the last of an odd stage count image 2, so
+// the image a stage writes was last read two barriers earlier).  Every LDS access of the step loop
+// is then one of five per-thread neighbour addresses plus an immediate offset: no address
+// arithmetic per stage.  Threads past the grid (the last wave's idle lanes) compute point 0's
+// stencil on their own zeros and write their garbage to the images' padding, so the step loop has
+// no branch either.
 // ---------------------------------------------------------------------------------------------
-// doubles per field image (half <= 1024).  At 1024 the u and v reads of a neighbour merge into one
-// ds_read2st64_b64 (and the two writes into one ds_write2st64_b64); measured the same as 1025 (ten
-// separate ds_read_b64): d = 800, 512 slices 6.34 / 6.35 us per RK8 step, 64 slices 3.66 / 3.67
-// (profiles/r03/field_probe_h.txt)
-static constexpr int FHN_PAIR_PS = 1024;
-
 template <int S> struct FhnPairImages {
     static constexpr int N = (S % 2 == 1 && S > 1) ? 3 : 2;
     // image of stage s (S == 1 alternates at run time)
@@ -456,6 +449,14 @@ __device__ __forceinline__ double fhn_sum5(const double (&v)[5], double k0, doub
     return s;
 }
 
+// Images interleaved [point][u, v], 16 bytes per point: a neighbour's u and v arrive by ONE
+// ds_read_b128 (4 LDS-array cycles per wave-instruction, 256 B/clk) and a point's two stage inputs
+// leave by one ds_write_b128.  Round 3's split [u | v] images needed a ds_read2st64_b64 (8 cycles,
+// 128 B/clk) per neighbour; PMC at 512 slices (profiles/r04/pmc_fhn_pair_r4c.txt) had the CU's LDS
+// ~70 % busy under it (66 LDS instructions per wave per RK8 step, 20 % of their cycles bank
+// conflicts) beside a 64 % busy VALU.  Measured (profiles/r04/fhn_pair_il_r4d.txt), us per RK8
+// step at d = 800: 512 slices 5.54 -> 4.91, 64 slices 3.53 -> 2.98; bitwise unchanged.  The image
+// stride is the block size (points past the grid write their own padding slots).
 template <int ORDER, bool LINSPACE, bool NORM>
 __global__ void __launch_bounds__(1024) rk_fhn_pair_kernel(FieldArgs fa, int n_slices,
                                                            const double *__restrict__ t0,
@@ -465,8 +466,8 @@ __global__ void __launch_bounds__(1024) rk_fhn_pair_kernel(FieldArgs fa, int n_s
                                                            double *__restrict__ uF) {
     using T = Tableau<ORDER>;
     using IM = FhnPairImages<T::S>;
-    constexpr int S = T::S, PS = FHN_PAIR_PS;
-    extern __shared__ __attribute__((aligned(16))) double smem[];   // [IM::N][2][PS]
+    constexpr int S = T::S;
+    extern __shared__ __attribute__((aligned(16))) double smem[];   // [IM::N][blockDim.x][2]
     const int slice = blockIdx.x;
     const int p = threadIdx.x;
     const int d = fa.d, half = d / 2;
@@ -500,20 +501,20 @@ __global__ void __launch_bounds__(1024) rk_fhn_pair_kernel(FieldArgs fa, int n_s
     double xw[2];
 #pragma unroll
     for (int r = 0; r < 2; r++) xw[r] = NORM ? (u[r] + 1) * w[r] + mn[r] : u[r];
+    const int ISTR = 2 * (int)blockDim.x;   // doubles per image
     for (int64_t n = 0; n < steps; n++) {
         const double h = LINSPACE ? grid.next(n, T0, T1, dt) : dt;
         double acc[2];   // sum_s b_s k_s, accumulated as the stages finish (step_update's order)
 #pragma unroll
         for (int s = 0; s < S; s++) {
             const int img = (S == 1) ? (int)(n & 1) : IM::of(s);
-            double *V = smem + img * 2 * PS;
-#pragma unroll
-            for (int r = 0; r < 2; r++) V[p + r * PS] = xw[r];
-            __syncthreads();
             double va[5], vb[5];
-            va[0] = V[nb.c0]; va[1] = V[nb.c1]; va[2] = V[nb.c2]; va[3] = V[nb.c3]; va[4] = V[nb.c4];
-            vb[0] = V[PS + nb.c0]; vb[1] = V[PS + nb.c1]; vb[2] = V[PS + nb.c2]; vb[3] = V[PS + nb.c3];
-            vb[4] = V[PS + nb.c4];
+            double2 *V2 = reinterpret_cast<double2 *>(smem + img * ISTR);
+            V2[p] = make_double2(xw[0], xw[1]);
+            __syncthreads();
+            const double2 w0 = V2[nb.c0], w1 = V2[nb.c1], w2 = V2[nb.c2], w3 = V2[nb.c3], w4 = V2[nb.c4];
+            va[0] = w0.x; va[1] = w1.x; va[2] = w2.x; va[3] = w3.x; va[4] = w4.x;
+            vb[0] = w0.y; vb[1] = w1.y; vb[2] = w2.y; vb[3] = w3.y; vb[4] = w4.y;
             // the next stage's input terms that do not involve this stage's k, computed while the
             // neighbour reads are in flight (pinned before the stencil: the reads' results pass
             // through the same empty asm, so LLVM can neither sink these sums past the stencil
@@ -788,7 +789,7 @@ static int launch_field(const nngp_system *sys, int n, const double *t0, const d
         const char *pe = getenv("NNGP_FHN_PAIR");
         if (!pe || atoi(pe) != 0) {
             const int bt = ((sys->d / 2 + 63) / 64) * 64;
-            const size_t lds = sizeof(double) * 2 * FHN_PAIR_PS * FhnPairImages<Tableau<ORDER>::S>::N;
+            const size_t lds = sizeof(double) * 2 * bt * FhnPairImages<Tableau<ORDER>::S>::N;
             if (fa.normalized)
                 hipLaunchKernelGGL((rk_fhn_pair_kernel<ORDER, LIN, true>), dim3(n), dim3(bt), lds, st, fa, n, t0, t1,
                                    steps, gsteps, j0, u0, uF);
