@@ -341,6 +341,39 @@ def gparareal_lorenz(torch, g):
                     'not the reference\'s own jax/XLA path'}
 
 
+def gparareal_burgers(torch, g):
+    """Full-data GParareal (model='gpjax', models.py:273-473) at BASELINE scale: Burgers d=128
+    N=128 T=5 on Burgers_perf_across_m.py's 2 000-step schedule.  Training rows grow to ~750; every
+    Nelder-Mead round factors one (rows+1)^2 matrix per unfinished fit of the d*9 = 1 152 (batched
+    blocked Cholesky, nngp_gpfull.hip).  The published GParareal run (Burges_scal_final_5_128_gp,
+    Burgers.py's paged schedule) converged in K = 6.  FP64 rate: the training's Cholesky flops,
+    sum over rounds of (active fits) x (rows+1)^3/3, are bounded above by 400 rounds x 1 152 fits
+    per call; the upper bound over the training time is reported against the FP64 peak."""
+    ode = g.Burgers(d_x=128, normalization='-11')
+    s = g.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
+    p = g.Parareal(ode, s, [0, 5], 128, epsilon=5e-7, verbose=None)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r = p.run(model='gpjax', add_model=True)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    mdl = r['mdl']
+    rows, K = [], r['k']
+    n_rows, I = 0, 0
+    for k in range(K):   # training rows at iteration k: sum over iterations of N - I_k + 1
+        n_rows += 128 - I + 1 - 1
+        rows.append(n_rows)
+        I = r['conv_int'][k] if k < len(r['conv_int']) else I
+    train = [float(v) for v in mdl.tot_train_t[:K]]
+    ub = sum(rd * 1152 * (n + 1) ** 3 / 3 for rd, n in zip(mdl.rounds, rows))
+    return {'wall_s': wall, 'K': K, 'reference_K': 6, 'converged': r['converged'], 'conv_int': list(r['conv_int']),
+            'F_time_s': r['timings']['F_time'], 'mdl_time_s': r['timings']['mdl_tot_t'],
+            'training_rows_per_iteration': rows, 'nm_rounds_per_iteration': list(mdl.rounds),
+            'training_s_per_iteration': train,
+            'cholesky_tflops_upper_bound': ub / max(sum(train), 1e-9) / 1e12,
+            'frac_fp64_peak_upper_bound': ub / max(sum(train), 1e-9) / 1e12 / FP64_PEAK_TFLOPS}
+
+
 def _oracle():
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import oracle as O
@@ -715,16 +748,19 @@ def sharded_sweep_timing(torch, g, solver, td, Ufull, Xd, Yd, rows, mdl, world, 
     gather = torch.zeros(world * chunk, dtype=torch.float64, device='cuda')
     comm = world > 1 and g._lib.comm_for(None)
 
+    send = torch.zeros(chunk, dtype=torch.float64, device='cuda')
+
     def python_loop():
         for i in range(n_sw):
             solver.run_G_batch(td[i:i + 1], td[i + 1:i + 2], U1[i:i + 1], out=UG1[i + 1:i + 2])
-            send = gather[rank * chunk:(rank + 1) * chunk]
             if c1 > c0:
                 g._lib.check(lib.nngp_predict_range(Xd.data_ptr(), Yd.data_ptr(), rows, d, U1[i].data_ptr(), m,
                                                     len(jit), jp, 1, th[i * nf:(i + 1) * nf].data_ptr(), c0, c1,
                                                     0.1, 0.1, 400, send.data_ptr(), st))
             if world > 1:
                 torch.distributed.all_gather_into_tensor(gather, send)
+            else:
+                gather.copy_(send)
             g._lib.check(lib.nngp_parareal_update(d, gather.data_ptr(), zeros.data_ptr(), UG1[i + 1].data_ptr(),
                                                   U1[i + 1].data_ptr(), st))
 
@@ -907,6 +943,8 @@ def main():
         log('published runs', json.dumps({k: res[k]['wall_s'] for k in ('burgers_n128_published_schedule_nngp',
                                                                          'tomlab_n256_configs_schedule_nngp')}))
         res['gparareal_lorenz_n32'] = gparareal_lorenz(torch, g)
+        res['gparareal_burgers_n128'] = gparareal_burgers(torch, g)
+        log('gparareal burgers', json.dumps(res['gparareal_burgers_n128']))
         log('gparareal lorenz K', res['gparareal_lorenz_n32']['K'], f"{res['gparareal_lorenz_n32']['wall_s']:.2f}s")
         res['burgers_n128_published_schedule'] = burgers_published_schedule(torch, g)
         res['tomlab_n256_published_schedule'] = tomlab_published_schedule(torch, g)

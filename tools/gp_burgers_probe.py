@@ -31,7 +31,7 @@ if __name__ == '__main__':
         p = g.Parareal(ode, s, [0, 5], 128, epsilon=5e-7, verbose=None)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    r = p.run(model='gpjax', early_stop=es)
+    r = p.run(model='gpjax', early_stop=es, add_model=True)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     tm = r['timings']
@@ -41,3 +41,7 @@ if __name__ == '__main__':
           f"G={tm['G_time']:.2f}s mdl={tm['mdl_tot_t']:.2f}s (train {tm['mdl_train_t']:.2f}s, pred {tm['mdl_pred_t']:.2f}s) "
           f"rows={r['x'].shape[0]}", flush=True)
     print('per-iteration max err', [f'{v:.3g}' for v in mx], flush=True)
+    mdl = r.get('mdl')
+    if mdl is not None:
+        print('Nelder-Mead rounds per training call', mdl.rounds, 'fits per call', 128 * 9,
+              'training seconds per iteration', [round(float(v), 3) for v in mdl.tot_train_t[:r['k']]], flush=True)
