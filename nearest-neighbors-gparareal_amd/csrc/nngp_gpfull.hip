@@ -12,14 +12,17 @@
 // factorisations of the (n+1) x (n+1) matrix [K; y^T] (row n rides along as a "row below", so the
 // factor's last row is z = L^-1 y and y.alpha = z.z):
 //   gpf_build_kernel   K of every point of the batch (lower triangle) from the hoisted D^2, + y^T
-//   gpf_panel_kernel   blocked right-looking Cholesky, panel j: a wave factors the 32x32 diagonal
-//                      block in registers (dpotf2 order), each thread solves one row below it
-//   gpf_syrk_kernel    trailing update A22 -= L21 L21^T, 32x32 lower tiles, LDS-staged panels
+//   gpf_diag_kernel    blocked right-looking Cholesky, panel j: one wave per matrix factors the
+//                      32x32 diagonal block in registers (dpotf2 order)
+//   gpf_rows_kernel    each thread solves one row below the diagonal block
+//   gpf_update_kernel  trailing update A22 -= L21 L21^T, 64x64 lower tiles, LDS-staged panels, on
+//                      the FP64 matrix cores (v_mfma_f64_16x16x4_f64)
 //   gpf_lml_kernel     -LML = 0.5 z.z + sum log L_ii + (n/2) log 2pi
 //   gpf_alpha_kernel   alpha = L^-T z for the posterior weights (once per fit() per coordinate)
-// FP64 VALU is the MI355X's FP64 peak (the FP64 MFMA rate is the same), so the tiles use plain
-// VALU FMAs.  The arithmetic order of LAPACK's blocked potrf is not reproduced (it is
-// third-party and build-dependent); parity is to tolerance (tests/test_gpu_gpfull.py).
+// The trailing update runs on the FP64 MFMA (same peak rate as the VALU, but operands come from
+// registers: two LDS reads per 1 024 multiply-adds instead of one per FMA).  The arithmetic order
+// of LAPACK's blocked potrf is not reproduced (it is third-party and build-dependent); parity is
+// to tolerance (tests/test_gpu_gpfull.py).
 // The Nelder-Mead state machines (nngp_nm.h, scipy's semantics) run on the host, one per fit.
 #include <cmath>
 #include <vector>
@@ -133,112 +136,203 @@ __device__ __forceinline__ bool diag_factor(double (&a)[GPB], double (&rinv)[GPB
     return true;
 }
 
-// Panel p0 (width pb).  Every workgroup of the matrix factors the diagonal block (wave 0, in
-// registers) and solves its 256 rows below it (rows p0+pb .. n, row n = y^T),
-// L21[r,:] = A21[r,:] L11^-T, right-looking with 1/L_jj (dtrsm's order); workgroup 0 leaves L11
-// in Lpan (the SYRK launch copies it into A, so no workgroup of this launch can read a
-// half-written diagonal block).
-__global__ void __launch_bounds__(256) gpf_panel_kernel(double *__restrict__ A, int n, int p0, int pb,
-                                                         int32_t *__restrict__ fail, double *__restrict__ Lpan) {
-    const int b = blockIdx.y;
+// Panel p0 (width pb), in two launches.
+// gpf_diag_kernel: ONE wave per matrix factors the diagonal block in registers (diag_factor) and
+// leaves L11 and 1/L_jj in Lpan[b] = [L11 (GPB x GPB, lower) | rinv (GPB)]; fail[b] on a failed
+// pivot.  (Round 3 factored it in every row-solve workgroup of the matrix, and the factor's ~190
+// VGPRs held the whole row-solve launch at two waves per SIMD: 118 us per panel at n = 753 with
+// 1 152 matrices, profiles/r04/gparareal_burgers_kernel_stats.csv.)
+// gpf_rows_kernel: every workgroup (one wave) stages its 64 rows below the block (rows p0+pb .. n,
+// row n = y^T) through LDS -- coalesced, a row's 32 doubles by consecutive lanes (one thread per
+// row reading its own row touched 64 cache lines per load instruction: 107 us per panel) -- and
+// solves L21[r,:] = A21[r,:] L11^-T, right-looking with 1/L_jj (dtrsm's order), L11 broadcast
+// from LDS (as wave-uniform scalar loads its 528 values spilled 920 SGPRs).  The update launch copies L11 into A, so no workgroup reads a half-written diagonal
+// block.
+static constexpr int LPS = GPB * GPB + GPB;   // Lpan doubles per matrix
+
+__global__ void __launch_bounds__(64) gpf_diag_kernel(const double *__restrict__ A, int n, int p0, int pb,
+                                                       int32_t *__restrict__ fail, double *__restrict__ Lpan) {
+    const int b = blockIdx.x;
     if (fail[b]) return;
     const int ld = n + 1;
-    double *Ab = A + (size_t)b * ld * ld;
-    __shared__ double L[GPB][GPB + 1];
-    __shared__ double Rv[GPB];
+    const double *Ab = A + (size_t)b * ld * ld;
     __shared__ double col[GPB];
-    __shared__ int bad;
-    const int tid = threadIdx.x;
-    if (tid < 64) {
-        const int i = tid;
-        double a[GPB], rv[GPB];
+    const int i = threadIdx.x;
+    double a[GPB], rv[GPB];
 #pragma unroll
-        for (int k = 0; k < GPB; k++) a[k] = (i < pb && k <= i) ? Ab[(size_t)(p0 + i) * ld + p0 + k] : 0.0;
-        const bool ok = diag_factor(a, rv, i, pb, col);
-        if (i == 0) bad = ok ? 0 : 1;
-        if (ok && i < GPB) {
-#pragma unroll
-            for (int k = 0; k < GPB; k++) L[i][k] = (i < pb && k <= i) ? a[k] : 0.0;
-            if (i == 0) {
-#pragma unroll
-                for (int k = 0; k < GPB; k++) Rv[k] = rv[k];
-            }
-        }
-    }
-    __syncthreads();
-    if (bad) {
-        if (tid == 0) fail[b] = 1;
+    for (int k = 0; k < GPB; k++) a[k] = (i < pb && k <= i) ? Ab[(size_t)(p0 + i) * ld + p0 + k] : 0.0;
+    const bool ok = diag_factor(a, rv, i, pb, col);
+    if (!ok) {
+        if (i == 0) fail[b] = 1;
         return;
     }
-    if (blockIdx.x == 0)
-        for (int t = tid; t < GPB * GPB; t += 256) Lpan[(size_t)b * GPB * GPB + t] = L[t / GPB][t % GPB];
-    const int r = p0 + pb + blockIdx.x * 256 + tid;
-    if (r > n) return;
-    double x[GPB];
-    double *row = Ab + (size_t)r * ld + p0;
+    double *Lb = Lpan + (size_t)b * LPS;
+    if (i < GPB) {
 #pragma unroll
-    for (int k = 0; k < GPB; k++) x[k] = k < pb ? row[k] : 0.0;
-#pragma unroll
-    for (int j = 0; j < GPB; j++) {
-        if (j < pb) {
-            x[j] = x[j] * Rv[j];
-#pragma unroll
-            for (int k = j + 1; k < GPB; k++)
-                if (k < pb) x[k] = x[k] - x[j] * L[k][j];
-        }
+        for (int k = 0; k < GPB; k++) Lb[i * GPB + k] = (i < pb && k <= i) ? a[k] : 0.0;
     }
+    if (i == 0) {
 #pragma unroll
-    for (int k = 0; k < GPB; k++)
-        if (k < pb) row[k] = x[k];
+        for (int k = 0; k < GPB; k++) Lb[GPB * GPB + k] = rv[k];
+    }
 }
 
-// trailing update below panel p0: A[i][j] -= sum_k L[i][p0+k] L[j][p0+k] for q0 <= j <= i <= n
-// (row n: the forward solve's update of y); workgroup = one 32x32 tile (ti >= tj), thread = 2x2
-// outputs.  The extra block ntiles copies the panel's L11 into A.
-__global__ void __launch_bounds__(256) gpf_syrk_kernel(double *__restrict__ A, int n, int p0, int pb,
-                                                        const int32_t *__restrict__ fail,
-                                                        const double *__restrict__ Lpan, int ntiles) {
+template <bool FULL>   // FULL: pb == GPB (every panel but a short last one) -- no per-column tests
+__global__ void __launch_bounds__(64) gpf_rows_kernel(double *__restrict__ A, int n, int p0, int pb,
+                                                       const int32_t *__restrict__ fail,
+                                                       const double *__restrict__ Lpan) {
     const int b = blockIdx.y;
     if (fail[b]) return;
     const int ld = n + 1;
     double *Ab = A + (size_t)b * ld * ld;
-    if ((int)blockIdx.x == ntiles) {
+    __shared__ double L[GPB * GPB + GPB];   // L11 | 1/L_jj (Lpan's layout)
+    __shared__ double X[64][GPB + 1];       // this wave's 64 rows of the panel, staged coalesced
+    const int tid = threadIdx.x;
+    const double *Lsrc = Lpan + (size_t)b * LPS;
+    const int r0 = p0 + pb + blockIdx.x * 64;
+    {   // every load issued before the first LDS write (rolled, one HBM round trip per 64 doubles)
+        constexpr int LU = (LPS + 63) / 64;
+        double lv[LU], xv[GPB];
+#pragma unroll
+        for (int u = 0; u < LU; u++) lv[u] = (tid + 64 * u < LPS) ? Lsrc[tid + 64 * u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < GPB; u++) {   // consecutive lanes read consecutive columns of a row
+            const int t = tid + 64 * u, rr = t / GPB, k = t % GPB;
+            xv[u] = (r0 + rr <= n && (FULL || k < pb)) ? Ab[(size_t)(r0 + rr) * ld + p0 + k] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < LU; u++)
+            if (tid + 64 * u < LPS) L[tid + 64 * u] = lv[u];
+#pragma unroll
+        for (int u = 0; u < GPB; u++) {
+            const int t = tid + 64 * u;
+            X[t / GPB][t % GPB] = xv[u];
+        }
+    }
+    const double *Lb = L;
+    __syncthreads();
+    double x[GPB];
+#pragma unroll
+    for (int k = 0; k < GPB; k++) x[k] = X[tid][k];
+#pragma unroll
+    for (int j = 0; j < GPB; j++) {
+        if (FULL || j < pb) {
+            x[j] = x[j] * Lb[GPB * GPB + j];
+#pragma unroll
+            for (int k = j + 1; k < GPB; k++)
+                if (FULL || k < pb) x[k] = x[k] - x[j] * Lb[k * GPB + j];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < GPB; k++) X[tid][k] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < GPB; u++) {
+        const int t = tid + 64 * u, rr = t / GPB, k = t % GPB;
+        if (r0 + rr <= n && (FULL || k < pb)) Ab[(size_t)(r0 + rr) * ld + p0 + k] = X[rr][k];
+    }
+}
+
+// Trailing update A[i][j] -= sum_{k < pb} L[i][p0+k] L[j][p0+k] (the factored panel's L columns)
+// over rows q0 <= i <= n (row n: the forward solve's update of y), columns q0 <= j < n, j <= i.
+// Workgroup = one 64x64 tile of the region's lower triangle (4 waves); the extra block `ntiles`
+// copies the L11 that Lpan holds into A.  The lane's 16 elements of A are loaded first, so their
+// HBM latency overlaps the rest; the tile's 64 + 64 panel rows are staged through LDS (row stride
+// GPB + 2 doubles: the 16 rows x 4 k of one MFMA operand read fall on distinct banks in each
+// 32-lane half), every load issued before the first LDS write; wave w multiplies its 16 rows by
+// the tile's 4 column blocks on the FP64 matrix cores (v_mfma_f64_16x16x4_f64: A[l&15][k + (l>>4)]
+// / B[k + (l>>4)][l&15] per lane; D col = l&15, row = (l>>4) + 4 reg).  Blocks j > i of a diagonal
+// tile are skipped.  Workgroups go round-robin over the 8 XCDs by linear id; the k-th workgroup of
+// XCD x takes matrix x + 8 (k / T), tile k % T (T = ntiles + 1, grid y padded to a multiple of 8),
+// so every tile of a matrix shares one L2.
+// Measured at Burgers N = 128 (profiles/r04/gparareal_burgers_r4*.txt): a rolled staging loop
+// (one HBM round trip per 256 elements) cost 25 %; two-panel look-ahead updates (64 L columns per
+// pass, half the trailing matrix's read-modify-write stream) were 5-30 % slower in every register
+// budget tried (the extra staging registers cost a wave per SIMD or spilled), so one panel per pass.
+// The accumulation order inside an MFMA k-step is the hardware's; GParareal's parity is to
+// tolerance and K (tests/test_gpu_gpfull.py), as LAPACK's blocked order is not reproduced anyway.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+static constexpr int GPF_TM = 64;              // update tile
+static constexpr int GPF_US = GPB + 2;         // LDS row stride of the staged panel rows
+
+__global__ void __launch_bounds__(256, 3) gpf_update_kernel(double *__restrict__ A, int n, int p0, int pb,
+                                                             const int32_t *__restrict__ fail,
+                                                             const double *__restrict__ Lpan, int ntiles, int nmat) {
+    const int T = ntiles + 1;
+    const int lin = blockIdx.x + blockIdx.y * T;
+    const int kx = lin >> 3;
+    const int b = (lin & 7) + 8 * (kx / T);
+    const int tile = kx % T;
+    if (b >= nmat || fail[b]) return;
+    const int ld = n + 1;
+    double *Ab = A + (size_t)b * ld * ld;
+    if (tile == ntiles) {
         for (int t = threadIdx.x; t < pb * pb; t += 256) {
             const int i = t / pb, j = t % pb;
-            if (j <= i) Ab[(size_t)(p0 + i) * ld + p0 + j] = Lpan[(size_t)b * GPB * GPB + i * GPB + j];
+            if (j <= i) Ab[(size_t)(p0 + i) * ld + p0 + j] = Lpan[(size_t)b * LPS + i * GPB + j];
         }
         return;
     }
+    int ti = (int)((sqrt(8.0 * tile + 1.0) - 1.0) / 2.0);
+    while ((ti + 1) * (ti + 2) / 2 <= tile) ti++;
+    while (ti * (ti + 1) / 2 > tile) ti--;
+    const int tj = tile - ti * (ti + 1) / 2;
     const int q0 = p0 + pb;
-    int ti = (int)((sqrt(8.0 * blockIdx.x + 1.0) - 1.0) / 2.0);
-    while ((ti + 1) * (ti + 2) / 2 <= (int)blockIdx.x) ti++;
-    while (ti * (ti + 1) / 2 > (int)blockIdx.x) ti--;
-    const int tj = blockIdx.x - ti * (ti + 1) / 2;
-    const int i0 = q0 + ti * 32, j0 = q0 + tj * 32;
-    __shared__ double Li[32][GPB + 1], Lj[32][GPB + 1];
+    const int i0 = q0 + ti * GPF_TM, j0 = q0 + tj * GPF_TM;
+    __shared__ double Li[GPF_TM * GPF_US], Lj[GPF_TM * GPF_US];
     const int tid = threadIdx.x;
-    for (int t = tid; t < 32 * GPB; t += 256) {
-        const int rr = t / GPB, k = t % GPB;
-        Li[rr][k] = (i0 + rr <= n && k < pb) ? Ab[(size_t)(i0 + rr) * ld + p0 + k] : 0.0;
-        Lj[rr][k] = (j0 + rr < n && k < pb) ? Ab[(size_t)(j0 + rr) * ld + p0 + k] : 0.0;
+    const int w = tid >> 6, lane = tid & 63;
+    const int kq = lane >> 4, ra = 16 * w + (lane & 15);
+    const int ncb = (ti == tj) ? w + 1 : 4;      // column blocks at or left of the diagonal
+    double old[4][4];
+#pragma unroll
+    for (int cb = 0; cb < 4; cb++) {
+        const int j = j0 + 16 * cb + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int i = i0 + 16 * w + kq + 4 * r;
+            old[cb][r] = (cb < ncb && i <= n && j < n && j <= i) ? Ab[(size_t)i * ld + j] : 0.0;
+        }
+    }
+    constexpr int SU = GPF_TM * GPB / 256;   // consecutive lanes: consecutive k of a row
+    double vi[SU], vj[SU];
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+        const int t = tid + 256 * u, rr = t / GPB, k = t % GPB;
+        vi[u] = (i0 + rr <= n && k < pb) ? Ab[(size_t)(i0 + rr) * ld + p0 + k] : 0.0;
+        vj[u] = (j0 + rr < n && k < pb) ? Ab[(size_t)(j0 + rr) * ld + p0 + k] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+        const int t = tid + 256 * u, rr = t / GPB, k = t % GPB;
+        Li[rr * GPF_US + k] = vi[u];
+        Lj[rr * GPF_US + k] = vj[u];
     }
     __syncthreads();
-    const int ri = (tid / 16) * 2, rj = (tid % 16) * 2;
-    double acc[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
-    for (int k = 0; k < pb; k++) {
-        const double a0 = Li[ri][k], a1 = Li[ri + 1][k], b0 = Lj[rj][k], b1 = Lj[rj + 1][k];
-        acc[0][0] = acc[0][0] + a0 * b0;
-        acc[0][1] = acc[0][1] + a0 * b1;
-        acc[1][0] = acc[1][0] + a1 * b0;
-        acc[1][1] = acc[1][1] + a1 * b1;
+    const int kend = (pb + 3) & ~3;              // the zero padding past pb adds exact zeros
+    f64x4 acc[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; cb++) acc[cb] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < GPB; k += 4) {
+        if (k >= kend) break;
+        const double av = Li[ra * GPF_US + k + kq];
+#pragma unroll
+        for (int cb = 0; cb < 4; cb++)
+            if (cb < ncb)
+                acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Lj[(16 * cb + (lane & 15)) * GPF_US + k + kq],
+                                                               acc[cb], 0, 0, 0);
     }
 #pragma unroll
-    for (int u = 0; u < 2; u++)
+    for (int cb = 0; cb < 4; cb++) {
+        if (cb >= ncb) continue;
+        const int j = j0 + 16 * cb + (lane & 15);
 #pragma unroll
-        for (int v = 0; v < 2; v++) {
-            const int i = i0 + ri + u, j = j0 + rj + v;
-            if (i <= n && j < n && j <= i) Ab[(size_t)i * ld + j] = Ab[(size_t)i * ld + j] - acc[u][v];
+        for (int r = 0; r < 4; r++) {
+            const int i = i0 + 16 * w + kq + 4 * r;
+            if (i <= n && j < n && j <= i) Ab[(size_t)i * ld + j] = old[cb][r] - acc[cb][r];
         }
+    }
 }
 
 __device__ __forceinline__ double block_sum(double v, double *red) {
@@ -369,14 +463,18 @@ static int gpf_eval(const double *D2, int n, const double *Y, int d, const GPPoi
     for (int p0 = 0; p0 < n; p0 += GPB) {
         const int pb = std::min(GPB, n - p0);
         const int below = n + 1 - p0 - pb;   // includes row n (y)
-        const unsigned chunks = (unsigned)std::max(1, (below + 255) / 256);
-        hipLaunchKernelGGL(gpf_panel_kernel, dim3(chunks, nb), dim3(256), 0, st, A, n, p0, pb, fail, Lpan);
-        NNGP_LAUNCH_CHECK();
-        const int nt = (below + 31) / 32, ntiles = nt * (nt + 1) / 2;
-        hipLaunchKernelGGL(gpf_syrk_kernel, dim3((unsigned)(ntiles + 1), nb), dim3(256), 0, st, A, n, p0, pb, fail,
-                           Lpan, ntiles);
-        NNGP_LAUNCH_CHECK();
+        const unsigned chunks = (unsigned)std::max(1, (below + 63) / 64);
+        hipLaunchKernelGGL(gpf_diag_kernel, dim3(nb), dim3(64), 0, st, A, n, p0, pb, fail, Lpan);
+        if (pb == GPB)
+            hipLaunchKernelGGL(gpf_rows_kernel<true>, dim3(chunks, nb), dim3(64), 0, st, A, n, p0, pb, fail, Lpan);
+        else
+            hipLaunchKernelGGL(gpf_rows_kernel<false>, dim3(chunks, nb), dim3(64), 0, st, A, n, p0, pb, fail, Lpan);
+        const int nt = (below + GPF_TM - 1) / GPF_TM;
+        const int ntiles = nt * (nt + 1) / 2;
+        const dim3 grid((unsigned)(ntiles + 1), (unsigned)((nb + 7) / 8 * 8));   // y padded: XCD order
+        hipLaunchKernelGGL(gpf_update_kernel, grid, dim3(256), 0, st, A, n, p0, pb, fail, Lpan, ntiles, nb);
     }
+    NNGP_LAUNCH_CHECK();
     hipLaunchKernelGGL(gpf_lml_kernel, dim3(nb), dim3(256), 0, st, A, n, fail, fval);
     NNGP_LAUNCH_CHECK();
     if (alpha_out) {
@@ -406,7 +504,7 @@ struct GPFWork {   // device buffers of one call
 static int gpf_workspace(int n, int nb, GPFWork &w) {
     int err = 0;
     const size_t nn = (size_t)n * n, mm = (size_t)(n + 1) * (n + 1);
-    const size_t bytes = sizeof(double) * (nn + (size_t)nb * mm + nb + (size_t)nb * GPB * GPB) + sizeof(GPPoint) * nb +
+    const size_t bytes = sizeof(double) * (nn + (size_t)nb * mm + nb + (size_t)nb * LPS) + sizeof(GPPoint) * nb +
                          sizeof(int32_t) * nb + 64;
     char *p = (char *)workspace(bytes, &err, 3);
     if (err) return err;
@@ -414,7 +512,7 @@ static int gpf_workspace(int n, int nb, GPFWork &w) {
     w.A = w.D2 + nn;
     w.fval = w.A + (size_t)nb * mm;
     w.Lpan = w.fval + nb;
-    w.pts = (GPPoint *)(w.Lpan + (size_t)nb * GPB * GPB);
+    w.pts = (GPPoint *)(w.Lpan + (size_t)nb * LPS);
     w.fail = (int32_t *)(w.pts + nb);
     return NNGP_OK;
 }

@@ -1,6 +1,6 @@
-// ubench_gpf.hip -- where the full-GP factorisation round spends its time (DESIGN.md §3.4):
+// ubench_gpf.hip -- where the full-GP factorisation round spends its time (DESIGN.md §3.5):
 // clock64 cycles of the 32x32 diagonal-block factor (one wave) and of one thread's 32-column row
-// solve, and HIP-event times of one panel / SYRK launch and one whole batched -LML evaluation.
+// solve, and HIP-event times of panel 0's diag + rows launches and one whole batched -LML evaluation.
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off -w tools/ubench_gpf.hip \
 //        -o scratch_bin/ubench_gpf
 #include "../nearest-neighbors-gparareal_amd/csrc/nngp_gpfull.hip"
@@ -8,6 +8,12 @@
 
 #include <cstdio>
 #include <vector>
+
+namespace nngp {   // nngp_shutdown's parts in the translation units this bench does not link
+void chain_release() {}
+void sweep_release() {}
+void comm_release() {}
+}  // namespace nngp
 
 using namespace nngp;
 
@@ -116,11 +122,12 @@ int main() {
         hipEventSynchronize(e1);
         float ms = 0;
         hipEventElapsedTime(&ms, e0, e1);
-        // panel 0 and SYRK 0 alone
+        // panel 0 alone (diagonal factor + row solve)
         hipEventRecord(e0, 0);
         for (int r = 0; r < 10; r++) {
             const int below = n + 1 - GPB;
-            hipLaunchKernelGGL(gpf_panel_kernel, dim3((below + 255) / 256, nb), dim3(256), 0, 0, w.A, n, 0, GPB,
+            hipLaunchKernelGGL(gpf_diag_kernel, dim3(nb), dim3(64), 0, 0, w.A, n, 0, GPB, w.fail, w.Lpan);
+            hipLaunchKernelGGL(gpf_rows_kernel<true>, dim3((below + 63) / 64, nb), dim3(64), 0, 0, w.A, n, 0, GPB,
                                w.fail, w.Lpan);
         }
         hipEventRecord(e1, 0);
