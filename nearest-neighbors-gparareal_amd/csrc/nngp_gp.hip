@@ -815,6 +815,9 @@ __device__ __forceinline__ double jit_lookup(const NMArgs &a, int j) {
 
 // register budget: MAXM <= 16 fits 256 VGPRs (<= 512 threads), MAXM <= 32 needs up to 512 (256);
 // MAXM > 32 (3-4 rows per lane) runs one wave per workgroup (LDS: four fit images, all registers)
+// (a 168-VGPR cap at MAXM <= 16 -- 3 waves per SIMD, a few spills -- made the Burgers batch fits
+// 12 % faster but starved the sweep's G launches running beside them: 0.258 -> 0.282 s end to end,
+// tools/sessions/r4n.sh)
 template <int MAXM> struct NMBound { static constexpr int T = (MAXM <= 16) ? 512 : (MAXM <= 32 ? 256 : 64); };
 // threads of the wave-per-fit speculative kernel and of the mean kernel
 template <int MAXM> struct WGT { static constexpr int T = MAXM > 32 ? 64 : 256; };
