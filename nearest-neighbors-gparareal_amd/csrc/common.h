@@ -66,13 +66,16 @@ constexpr int N_WS_SLOTS = 10;   // slot 2: the sweep's speculation buffers; 3: 
                                 // 9: the sharded sweep's zeros (nngp_comm.hip)
 void *workspace(size_t bytes, int *err, int slot = 0);
 
+// predict_impl's launches in parts (the speculative sweep issues the select, reads its hit flag on
+// the host, and then launches the fits only on a miss): all | kNN + select | fits + mean | mean only
+enum { PREDICT_ALL = 0, PREDICT_SELECT = 1, PREDICT_FITS_MEAN = 2, PREDICT_MEAN = 3 };
 int predict_impl(const double *X, const double *Y, int64_t rows, int d, const double *new_x, int m,
                  int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
                  double fatol, double xatol, int maxfev, double *preds_out, const double *bias,
                  double *out, double *fits_out, const int32_t *spec_idx, const double *spec_fits,
                  int32_t *hit_flag, const int32_t *spec2_idx, const double *spec2_fits, int32_t *host_flag,
                  hipStream_t st, int c0 = 0, int c1 = -1, const int32_t *wait_done = nullptr,
-                 int32_t *wait_err = nullptr);
+                 int32_t *wait_err = nullptr, int phase = PREDICT_ALL);
 int gpfull_mean(const double *X, int64_t rows, int d, const double *q, const double *coef, const double *alpha,
                 const double *bias, double *out, hipStream_t st);
 int spec_batch(const double *X, const double *Y, int64_t rows, int d, const double *Q, int nq, int m,
@@ -86,6 +89,9 @@ void comm_release();
 // grow-only pool of timing events (nngp_sweep.hip): *out = n events
 int timing_events(size_t n, hipEvent_t **out);
 bool chain_supported(const nngp_system *sys, int g_step_mode, int m);
+bool guess_chain_supported(const nngp_system *sys, int g_step_mode);
+int guess_chain(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps, const double *t, int I,
+                int nq, const double *UF, const double *UG, double *Q, double *gtmp, hipStream_t st);
 int chain_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps, const double *t, int I,
                 int N, int i0, double *U1, double *UG1, const double *X, const double *Y, int64_t rows, int m,
                 int n_jitter, const double *jitter_exp_host, int n_restarts, int32_t *flags,

@@ -153,7 +153,10 @@ __device__ __forceinline__ double knn_dist_row(const double *__restrict__ X, int
     double acc = 0.0;
     int c = 0;
     if ((((uintptr_t)xr | (uintptr_t)q) & 15) == 0) {   // 16-byte aligned rows: double2 loads
-        constexpr int B = 32;                            // 32 loads in flight per lane
+        // 16 double2 loads in flight per lane: 74 VGPRs, so a sweep's kNN launch fits beside the
+        // overlapped batch's fit waves (2 per SIMD at 192 VGPRs); at 32 in flight (139 VGPRs) it
+        // waited ~3 ms for a SIMD to drain at the start of each Burgers iteration
+        constexpr int B = 16;
         for (; c + 2 * B <= d; c += 2 * B) {
             double2 v[B];
 #pragma unroll
@@ -2042,8 +2045,9 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
                  double fatol, double xatol, int maxfev, double *preds_out, const double *bias,
                  double *out, double *fits_out, const int32_t *spec_idx, const double *spec_fits,
                  int32_t *hit_flag, const int32_t *spec2_idx, const double *spec2_fits, int32_t *host_flag,
-                 hipStream_t st, int c0, int c1, const int32_t *wait_done, int32_t *wait_err) {
+                 hipStream_t st, int c0, int c1, const int32_t *wait_done, int32_t *wait_err, int phase) {
     NNGP_REQUIRE(X && Y && new_x && theta0 && preds_out, "null array argument");
+    NNGP_REQUIRE(phase >= PREDICT_ALL && phase <= PREDICT_MEAN, "bad predict phase %d", phase);
     if (c1 < 0) c1 = d;
     NNGP_REQUIRE(0 <= c0 && c0 < c1 && c1 <= d, "bad coordinate range [%d, %d) of d=%d", c0, c1, d);
     NNGP_REQUIRE(m >= 1 && m <= MAX_M, "need 1 <= m <= %d (got %d)", MAX_M, m);
@@ -2066,20 +2070,23 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
     double *ymT = kd2 + m;
     int32_t *idx = (int32_t *)(ymT + (size_t)d * m);
     double *fits_ws = (double *)(ws + sizeof(double) * nd + sizeof(int32_t) * 64);
-    hipLaunchKernelGGL(knn_dist_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, X, rows,
-                       d, new_x, dist);
-    NNGP_LAUNCH_CHECK();
-    const bool wave_d2 = d2_by_waves(m, d);
-    launch_knn_select(dim3(1), knn_xs_bytes(m, d), st, dist, rows, m, X, Y, d, new_x, idx, (double *)nullptr,
-                      ymT, wave_d2 ? (double *)nullptr : D2, wave_d2 ? (double *)nullptr : kd2,
-                      spec ? spec_idx : (const int32_t *)nullptr,
-                      spec ? hit_flag : (int32_t *)nullptr, knn_xs_doubles(m, d),
-                      spec ? spec2_idx : (const int32_t *)nullptr, spec ? host_flag : (int32_t *)nullptr);
-    NNGP_LAUNCH_CHECK();
-    if (wave_d2) {
-        hipLaunchKernelGGL(d2_wave_kernel, dim3((unsigned)(m * (m + 1) / 2 + m)), dim3(64), 0, st, X, idx, m, d,
-                           new_x, D2, kd2);
+    if (phase == PREDICT_ALL || phase == PREDICT_SELECT) {
+        hipLaunchKernelGGL(knn_dist_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, X, rows,
+                           d, new_x, dist);
         NNGP_LAUNCH_CHECK();
+        const bool wave_d2 = d2_by_waves(m, d);
+        launch_knn_select(dim3(1), knn_xs_bytes(m, d), st, dist, rows, m, X, Y, d, new_x, idx, (double *)nullptr,
+                          ymT, wave_d2 ? (double *)nullptr : D2, wave_d2 ? (double *)nullptr : kd2,
+                          spec ? spec_idx : (const int32_t *)nullptr,
+                          spec ? hit_flag : (int32_t *)nullptr, knn_xs_doubles(m, d),
+                          spec ? spec2_idx : (const int32_t *)nullptr, spec ? host_flag : (int32_t *)nullptr);
+        NNGP_LAUNCH_CHECK();
+        if (wave_d2) {
+            hipLaunchKernelGGL(d2_wave_kernel, dim3((unsigned)(m * (m + 1) / 2 + m)), dim3(64), 0, st, X, idx, m,
+                               d, new_x, D2, kd2);
+            NNGP_LAUNCH_CHECK();
+        }
+        if (phase == PREDICT_SELECT) return NNGP_OK;
     }
     // coordinates [c0, c1) only (the multi-rank sweep's share): the fits and means of those
     // columns, in the same product(coord, jitter, restart) order with their own theta0 draws
@@ -2102,6 +2109,10 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
             const double us = std::max(0, env_int("NNGP_SPEC_WAIT_US", 2000000));
             a.wait_ticks = (uint64_t)(us * device_wallclock_khz() / 1e3);
         }
+    }
+    if (phase == PREDICT_MEAN) {   // the select's hit is known: the fits are the speculative batch's
+        NNGP_REQUIRE(spec, "predict: the mean-only phase needs the speculative fits");
+        return run_mean(a, st);
     }
     if (use_spec(a.n_fits, a.m)) {   // fits (a wave each), then arg-min + mean (+ bias) per coordinate
         rc = run_nm_spec(a, st);
@@ -2212,6 +2223,106 @@ static int chain_resources(ChainRes **out) {
     return NNGP_OK;
 }
 
+// G of one slice in-kernel (the chain and the guess chain): the G launch's system, tableau and grid
+struct GArgs {
+    LaneArgs la;    // an ODE (gkind 0): one lane
+    FieldArgs fa;   // Burgers (gkind 1): one wave, d = 64 * ept
+    int gkind, sys, order, lin, norm, ept;
+    int64_t g_steps;
+};
+
+static int g_args(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps, GArgs &g) {
+    g = GArgs{};
+    const int d = sys->d, kind = sys->kind;
+    if (kind == NNGP_SYS_BURGERS) {
+        g.gkind = 1;
+        g.ept = d / 64;
+        g.fa.d = d; g.fa.nx = sys->nx; g.fa.normalized = sys->normalized; g.fa.norm = sys->norm;
+        const double dx = (1.0 - (-1.0)) / (sys->d - 1);   // as field_args (nngp_rk_dev.h users)
+        const double nu = sys->param[0];
+        g.fa.c_off = nu / (dx * dx);
+        g.fa.c_diag = g.fa.c_off * -2.0;
+        g.fa.c_grad = 1 / (2 * dx);
+    } else {
+        g.gkind = 0;
+        g.la.normalized = sys->normalized;
+        for (int k = 0; k < 4; k++) g.la.param[k] = sys->param[k];
+        g.la.rparam0 = 1.0 / sys->param[0];
+        g.la.norm = sys->norm;
+    }
+    NNGP_REQUIRE(!sys->normalized || sys->norm, "normalized system needs norm[3d]");
+    NNGP_REQUIRE(g_tableau == 1 || g_tableau == 2 || g_tableau == 4 || g_tableau == 8, "bad G tableau %d", g_tableau);
+    g.sys = kind; g.order = g_tableau;
+    g.lin = (g_step_mode & ~NNGP_STEP_CONTRACT) == NNGP_STEP_LINSPACE;
+    g.norm = sys->normalized != 0;
+    g.g_steps = g_steps;
+    return NNGP_OK;
+}
+
+// systems whose G runs in-kernel: every ODE (lane form) and Burgers with d = 64*EPT <= 256 (wave
+// form); exact G only (the contracted build's G is another kernel)
+static bool g_in_kernel(const nngp_system *sys, int g_step_mode) {
+    if (g_step_mode & NNGP_STEP_CONTRACT) return false;
+    switch (sys->kind) {
+    case NNGP_SYS_LORENZ: case NNGP_SYS_HOPF: case NNGP_SYS_THOMAS_LABYRINTH: case NNGP_SYS_FHN_ODE:
+    case NNGP_SYS_ROSSLER: case NNGP_SYS_BRUSSELATOR: case NNGP_SYS_DBL_PEND:
+        return true;
+    case NNGP_SYS_BURGERS:
+        return sys->nx == sys->d && sys->d % 64 == 0 && sys->d <= CHAIN_QMAX;
+    default:
+        return false;
+    }
+}
+
+// The speculative sweep's guesses along the coarse chain (nngp_sweep.hip), ONE wave for all of them:
+//   Q[j+1] = (UF[I+j+1] - UG[I+j+1]) + G(Q[j]),   j = 0 .. nq-2
+// with the G launch's own device code (lane_slice / burgers_wave_slice) and nngp_parareal_update's
+// expression, so Q is bitwise the launch loop's (2 launches per slice: ~19 us of host issue each
+// pair, 2.4 ms per Burgers N = 128 iteration).  Every element is written and re-read by the lane
+// that owns it (lane 0 for an ODE, lane l for Burgers elements l*ept ..), so no barrier is needed.
+__global__ void __launch_bounds__(64) guess_chain_kernel(GArgs g, const double *__restrict__ t, int I, int nq, int d,
+                                                         const double *__restrict__ UF, const double *__restrict__ UG,
+                                                         double *Q, double *gtmp) {
+    const int l = threadIdx.x;
+    for (int j = 0; j + 1 < nq; j++) {
+        const int i = I + j;
+        const double *q = Q + (size_t)j * d;
+        double *qn = Q + (size_t)(j + 1) * d;
+        const double *uf = UF + (size_t)(i + 1) * d, *ug = UG + (size_t)(i + 1) * d;
+        if (g.gkind == 1) {
+            chain_burgers_g(g.fa, g.ept, g.order, g.lin, g.norm, l, t[i], t[i + 1], g.g_steps, q, gtmp);
+            for (int r = 0; r < g.ept; r++) {
+                const int e = l * g.ept + r;
+                const double p = uf[e] - ug[e];
+                qn[e] = p + gtmp[e];
+            }
+        } else if (l == 0) {
+            chain_lane_g(g.la, g.sys, g.order, g.lin, g.norm, t[i], t[i + 1], g.g_steps, q, gtmp);
+            for (int e = 0; e < d; e++) {
+                const double p = uf[e] - ug[e];
+                qn[e] = p + gtmp[e];
+            }
+        }
+    }
+}
+
+// false: the caller keeps the launch loop (a system without in-kernel G, or NNGP_GUESS_FUSED=0)
+bool guess_chain_supported(const nngp_system *sys, int g_step_mode) {
+    return env_int("NNGP_GUESS_FUSED", 1) != 0 && g_in_kernel(sys, g_step_mode);
+}
+
+int guess_chain(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps, const double *t, int I,
+                int nq, const double *UF, const double *UG, double *Q, double *gtmp, hipStream_t st) {
+    NNGP_REQUIRE(g_in_kernel(sys, g_step_mode), "guess chain: no in-kernel G for this system");
+    if (nq < 2) return NNGP_OK;
+    GArgs g;
+    const int rc = g_args(sys, g_tableau, g_step_mode, g_steps, g);
+    if (rc) return rc;
+    hipLaunchKernelGGL(guess_chain_kernel, dim3(1), dim3(64), 0, st, g, t, I, nq, sys->d, UF, UG, Q, gtmp);
+    NNGP_LAUNCH_CHECK();
+    return NNGP_OK;
+}
+
 // the systems / shapes the chain's in-kernel G covers (the rest keep the launch chain):
 // every ODE (lane form) and Burgers with d = 64*EPT <= 256 (wave form); exact G, m <= 24 (at the
 // padded size 32 the mean phase's 16 fit images -- K/L plus the per-row scalars -- and the select's
@@ -2221,17 +2332,8 @@ static int chain_resources(ChainRes **out) {
 bool chain_supported(const nngp_system *sys, int g_step_mode, int m) {
     const char *e = getenv("NNGP_CHAIN");
     if (!e || atoi(e) == 0) return false;
-    if (g_step_mode & NNGP_STEP_CONTRACT) return false;
     if (m < 1 || m > 24 || sys->d > CHAIN_QMAX) return false;
-    switch (sys->kind) {
-    case NNGP_SYS_LORENZ: case NNGP_SYS_HOPF: case NNGP_SYS_THOMAS_LABYRINTH: case NNGP_SYS_FHN_ODE:
-    case NNGP_SYS_ROSSLER: case NNGP_SYS_BRUSSELATOR: case NNGP_SYS_DBL_PEND:
-        return true;
-    case NNGP_SYS_BURGERS:
-        return sys->nx == sys->d && sys->d % 64 == 0 && sys->d <= 256;
-    default:
-        return false;
-    }
+    return g_in_kernel(sys, g_step_mode);
 }
 
 // An ordinary launch.  The grid barrier needs every workgroup resident at once: nb <= 64
@@ -2278,29 +2380,11 @@ int chain_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t 
     double *D2 = dist + rows, *kd2 = D2 + (size_t)m * m, *ymT = kd2 + m;
     c.a.m = m; c.a.d = d; c.a.n_fits = (int)n_fits; c.a.D2 = D2; c.a.kd2 = kd2; c.a.Y = ymT;
     c.a.ys_c = m; c.a.ys_r = 1; c.a.R = n_restarts;
-    const int kind = sys->kind;
-    if (kind == NNGP_SYS_BURGERS) {
-        c.gkind = 1;
-        c.ept = d / 64;
-        c.fa.d = d; c.fa.nx = sys->nx; c.fa.normalized = sys->normalized; c.fa.norm = sys->norm;
-        const double dx = (1.0 - (-1.0)) / (sys->d - 1);   // as field_args (nngp_rk_dev.h users)
-        const double nu = sys->param[0];
-        c.fa.c_off = nu / (dx * dx);
-        c.fa.c_diag = c.fa.c_off * -2.0;
-        c.fa.c_grad = 1 / (2 * dx);
-    } else {
-        c.gkind = 0;
-        c.la.normalized = sys->normalized;
-        for (int k = 0; k < 4; k++) c.la.param[k] = sys->param[k];
-        c.la.rparam0 = 1.0 / sys->param[0];
-        c.la.norm = sys->norm;
-    }
-    NNGP_REQUIRE(!sys->normalized || sys->norm, "normalized system needs norm[3d]");
-    NNGP_REQUIRE(g_tableau == 1 || g_tableau == 2 || g_tableau == 4 || g_tableau == 8, "bad G tableau %d", g_tableau);
-    c.sys = kind; c.order = g_tableau;
-    c.lin = (g_step_mode & ~NNGP_STEP_CONTRACT) == NNGP_STEP_LINSPACE;
-    c.norm = sys->normalized != 0;
-    c.g_steps = g_steps;
+    GArgs ga;
+    rc = g_args(sys, g_tableau, g_step_mode, g_steps, ga);
+    if (rc) return rc;
+    c.la = ga.la; c.fa = ga.fa; c.gkind = ga.gkind; c.ept = ga.ept;
+    c.sys = ga.sys; c.order = ga.order; c.lin = ga.lin; c.norm = ga.norm; c.g_steps = ga.g_steps;
     c.t = t; c.I = I; c.N = N; c.i0 = i0;
     c.U1 = U1; c.UG1 = UG1; c.X = X; c.Yd = Y; c.rows = rows;
     const int64_t per = (rows + 255) / 256;

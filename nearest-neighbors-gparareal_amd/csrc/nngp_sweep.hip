@@ -229,6 +229,9 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
             for (int64_t j = 0; j < nq; j++) rs->hflags[j] = -1;
         }
         NNGP_HIP_CHECK(hipMemcpyAsync(Qg, U1 + (size_t)I * d, sizeof(double) * d, hipMemcpyDeviceToDevice, st));
+        if (guess_chain_supported(sys, g_step_mode))   // one launch for the whole chain (bitwise)
+            rc = guess_chain(sys, g_tableau, g_step_mode, g_steps, t, I, (int)nq, UF, UG, Qg, gtmp, st);
+        else
         for (int64_t j = 0; j + 1 < nq && rc == NNGP_OK; j++) {
             const int i = I + (int)j;
             rc = nngp_rk_batch(sys, g_tableau, g_step_mode, 1, t + i, t + i + 1, g_steps, Qg + j * d, gtmp, stream);
@@ -322,17 +325,28 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
             if (respec_pending) NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_r, 0));   // lists/fits ready
             respec_pending = false;
         }
-        rc = predict_impl(X, Y, rows, d, ui, m, n_jitter, jitter_exp_host, n_restarts, theta0 + j * n_fits * 2, fatol,
-                          xatol, maxfev, preds_scratch, ug_next, u_next, nullptr, spec ? spec_idx + j * m : nullptr,
-                          spec ? spec_fits + j * n_fits * 4 : nullptr, spec ? flags + j : nullptr,
-                          W > 0 ? spec2_idx + j * m : nullptr, W > 0 ? spec2_fits + j * n_fits * 4 : nullptr,
-                          (W > 0 && i + 1 < N) ? rs->hflags + j : nullptr, st, 0, -1,   // every written flag is awaited
-                          overlap ? done + j : nullptr, overlap ? rs->herr : nullptr);
-        if (rc || W == 0 || i + 1 >= N) continue;
+        // with a host flag (W > 0, not the last slice) the prediction is issued in two parts: the
+        // kNN + select, then -- once the host has read the select's hit code -- the mean alone on a
+        // hit (the fits are the batch's) or the fits and the mean on a miss.  The fits launch a hit
+        // would have skipped on the device is never issued: its waves (191 VGPRs) could only be
+        // dispatched once the overlapped batch's waves drained a SIMD.
+        const bool split = spec && W > 0 && i + 1 < N;
+        auto predict = [&](int phase) {
+            return predict_impl(X, Y, rows, d, ui, m, n_jitter, jitter_exp_host, n_restarts, theta0 + j * n_fits * 2,
+                                fatol, xatol, maxfev, preds_scratch, ug_next, u_next, nullptr,
+                                spec ? spec_idx + j * m : nullptr, spec ? spec_fits + j * n_fits * 4 : nullptr,
+                                spec ? flags + j : nullptr, W > 0 ? spec2_idx + j * m : nullptr,
+                                W > 0 ? spec2_fits + j * n_fits * 4 : nullptr,
+                                split ? rs->hflags + j : nullptr, st, 0, -1,   // every written flag is awaited
+                                overlap ? done + j : nullptr, overlap ? rs->herr : nullptr, phase);
+        };
+        rc = predict(split ? PREDICT_SELECT : PREDICT_ALL);
+        if (rc || !split) continue;
         int32_t hit = 0;
         rc = wait_flag(rs->hflags + j, st, &hit);
         // a mean that gave up waiting for the overlapped batch: stop issuing, the caller reruns
         if (rc == NNGP_OK && overlap && __atomic_load_n(rs->herr, __ATOMIC_ACQUIRE) != 0) break;
+        if (rc == NNGP_OK) rc = predict(hit != 0 ? PREDICT_MEAN : PREDICT_FITS_MEAN);
         if (rc || hit != 0) continue;
         // miss: re-guess slices i+1 .. i+w from the actual U1[i] on the side stream
         const int w = (int)std::min<int64_t>(W, N - 1 - i);

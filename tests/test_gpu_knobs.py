@@ -39,7 +39,8 @@ KNOBS = [
     ('fhn512', 'NNGP_FHN_PAIR', '0'), ('fhn512', 'NNGP_NM_PARK', '0'), ('fhn512', 'NNGP_NM_PARK', '20'),
     ('fhn512', 'NNGP_RK_THREADS', '512'), ('lorenz', 'NNGP_RK_GROUP', '0'), ('lorenz', 'NNGP_CHAIN', '1'),
     ('lorenz', 'NNGP_NM_LEVEL2', '0'), ('fhn512', 'NNGP_RESUME_W4', '0'), ('fhn512', 'NNGP_RESUME_W4', '100000'),
-    ('fhn512', 'NNGP_RESUME_W2', '0'), ('burgers', 'NNGP_SPEC_WAIT_US', '0'),
+    ('fhn512', 'NNGP_RESUME_W2', '0'), ('burgers', 'NNGP_SPEC_WAIT_US', '0'), ('burgers', 'NNGP_GUESS_FUSED', '0'),
+    ('lorenz', 'NNGP_GUESS_FUSED', '0'),
 ]
 
 

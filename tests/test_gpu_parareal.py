@@ -166,6 +166,36 @@ def test_speculative_sweep_is_bitwise_and_hits(gpu, case, window, monkeypatch):
     assert sum(hits) > 0 and a['timings']['spec_hits'] == [0] * len(hits)
 
 
+@pytest.mark.parametrize('case', ['burgers', 'hopf', 'tomlab'])
+def test_fused_guess_chain_keeps_hits_and_bits(gpu, case, monkeypatch):
+    """The speculative sweep's guesses along the coarse chain by one wave (guess_chain_kernel,
+    NNGP_GUESS_FUSED=1, default) against the launch loop (G + update per slice): the same guesses bit
+    for bit show as the same speculation hits in every iteration, and the run is bitwise unchanged."""
+    if case == 'burgers':      # wave form of G (d = 128, RK1, normalised)
+        ode = gpu.Burgers(d_x=128, normalization='-11')
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
+        p = gpu.Parareal(ode, s, [0, 5], 128, epsilon=5e-7, verbose=None)
+        kw = dict(nn=15, seed=45, early_stop=4)
+    elif case == 'hopf':       # lane form, the Markstein division (RK4 G)
+        ode = gpu.Hopf(normalization='-11')
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=16, Nf=1360, F='RK4', G='RK4')
+        p = gpu.Parareal(ode, s, [-20, 500], 128, epsilon=5e-7, verbose=None)
+        kw = dict(nn=11, seed=45, early_stop=4)
+    else:                      # lane form with nn_sin_pi (RK4 G)
+        ode = gpu.ThomasLabyrinth(normalization='-11')
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=10, Nf=3910, F='RK4', G='RK4')
+        p = gpu.Parareal(ode, s, [0, 10], 64, epsilon=5e-7, verbose=None)
+        kw = dict(nn=11, seed=45, early_stop=4)
+    monkeypatch.setenv('NNGP_GUESS_FUSED', '0')
+    a = p.run(model='nngp', **kw)
+    monkeypatch.setenv('NNGP_GUESS_FUSED', '1')
+    b = p.run(model='nngp', **kw)
+    print(case, 'hits launch loop', a['timings']['spec_hits'], 'fused', b['timings']['spec_hits'])
+    assert a['timings']['spec_hits'] == b['timings']['spec_hits'] and sum(b['timings']['spec_hits']) > 0
+    assert a['k'] == b['k'] and a['conv_int'] == b['conv_int']
+    assert np.array_equal(np.nan_to_num(a['u'], nan=7.0), np.nan_to_num(b['u'], nan=7.0))
+
+
 def test_run_kwargs_override_constructor_settings(gpu):
     """run(..., speculate=...) applies to that run only (the constructor's value otherwise)."""
     ode = gpu.Lorenz(normalization='-11')
