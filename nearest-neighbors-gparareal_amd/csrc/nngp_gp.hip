@@ -273,6 +273,11 @@ static inline size_t knn_xs_bytes(int m, int64_t d) { return (size_t)knn_xs_doub
 static inline bool d2_by_waves(int m, int d) {
     return env_int("NNGP_D2_WAVES", 1) != 0 && (d > 128 || knn_xs_doubles(m, d) == 0);
 }
+// D2 / kd2 by d2_pairs_kernel (one thread per pair): the cases neither the select kernel (rows
+// staged, d <= 128) nor the wave-per-pair kernel (NNGP_D2_WAVES=0) takes
+static inline bool d2_by_pairs(int m, int d) {
+    return !d2_by_waves(m, d) && (d > 128 || knn_xs_doubles(m, d) == 0);
+}
 
 // LDS of one select (the caller's: a kernel-level __shared__ object, one per kernel)
 static constexpr int SEL_CAND = 256;   // candidates the threshold select ranks exactly
@@ -349,7 +354,7 @@ __device__ __forceinline__ double pw_leaf_octet(const double *__restrict__ a, co
 // spec_idx / hit_flag (single query): hit_flag = 1 iff the selected ordered neighbour list equals
 // spec_idx, else 2 iff it equals spec2_idx (when given), else 0 -- the speculative sweep then
 // reuses the fits it computed for that list.  host_flag (host-mapped, optional) gets the same value.
-template <int K>
+template <int K, bool GENERIC_D2 = true>
 __device__ __forceinline__ void knn_select_dev(
     SelShm &sh, const double *__restrict__ dist, int64_t rows, int m, const double *__restrict__ X,
     const double *__restrict__ Y, int d, const double *__restrict__ q, int32_t *__restrict__ idx_out,
@@ -616,7 +621,7 @@ __device__ __forceinline__ void knn_select_dev(
                     }
                 }
             }
-        } else
+        } else if constexpr (GENERIC_D2) {   // the fused chain: any d, staged or not
         for (int t = tid; t < ntask; t += 256) {
             if (t >= npairs) {
                 const int r = t - npairs;
@@ -631,6 +636,31 @@ __device__ __forceinline__ void knn_select_dev(
             const double v = pw_sqdiff(xr, xj, d);
             D2[r * m + j] = v;
             D2[j * m + r] = v;
+        }
+        } else {   // d < 8, staged (the host's contract for this kernel): pw_leaf's sequential branch
+        for (int t = tid; t < ntask; t += 256) {
+            int r = 0, j = 0;
+            const double *xj = q;
+            if (t >= npairs) {
+                r = t - npairs;
+            } else {
+                while ((r + 1) * (r + 2) / 2 <= t) r++;
+                j = t - r * (r + 1) / 2;
+                xj = xs + (size_t)j * ds;
+            }
+            const double *xr = xs + (size_t)r * ds;
+            double res = 0.;
+            for (int i = 0; i < d; i++) {
+                const double u = xr[i] - xj[i];
+                res += u * u;
+            }
+            if (t >= npairs) {
+                kd2[r] = res;
+            } else {
+                D2[r * m + j] = res;
+                D2[j * m + r] = res;
+            }
+        }
         }
     }
     __syncthreads();
@@ -654,8 +684,38 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
     if (ymT) ymT += (size_t)qy * d * m;
     if (D2) D2 += (size_t)qy * m * m;
     if (kd2) kd2 += (size_t)qy * m;
-    knn_select_dev<K>(sh, dist, rows, m, X, Y, d, q, idx_out, dist_out, ymT, D2, kd2, spec_idx, hit_flag,
+    knn_select_dev<K, false>(sh, dist, rows, m, X, Y, d, q, idx_out, dist_out, ymT, D2, kd2, spec_idx, hit_flag,
                       xs_doubles, spec2_idx, host_flag);
+}
+
+// D2 / kd2 of the selected rows by one thread per pair (pw_sqdiff, reading X): the select's former
+// in-kernel path for rows it cannot stage or d > 128, kept for NNGP_D2_WAVES=0 (query blockIdx.y;
+// kd2 may be null).  Out of the select kernel its recursion stack no longer sets the select's
+// register count (288 VGPRs with it, ~40 without: the select then fits beside the overlapped
+// batch's fit waves).
+__global__ void __launch_bounds__(256) d2_pairs_kernel(const double *__restrict__ X, const int32_t *__restrict__ idx,
+                                                       int m, int d, const double *__restrict__ q,
+                                                       double *__restrict__ D2, double *__restrict__ kd2) {
+    const int qy = blockIdx.y;
+    idx += (size_t)qy * m;
+    q += (size_t)qy * d;
+    D2 += (size_t)qy * m * m;
+    if (kd2) kd2 += (size_t)qy * m;
+    const int npairs = m * (m + 1) / 2;
+    const int ntask = npairs + (kd2 ? m : 0);
+    for (int t = blockIdx.x * 256 + threadIdx.x; t < ntask; t += gridDim.x * 256) {
+        if (t >= npairs) {
+            const int r = t - npairs;
+            kd2[r] = pw_sqdiff(X + (int64_t)idx[r] * d, q, d);
+            continue;
+        }
+        int r = 0;
+        while ((r + 1) * (r + 2) / 2 <= t) r++;
+        const int j = t - r * (r + 1) / 2;
+        const double v = pw_sqdiff(X + (int64_t)idx[r] * d, X + (int64_t)idx[j] * d, d);
+        D2[r * m + j] = v;
+        D2[j * m + r] = v;
+    }
 }
 
 // D2 / kd2 of the m selected rows when d > 128 or the rows do not fit the select's LDS staging:
@@ -2074,9 +2134,10 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
         hipLaunchKernelGGL(knn_dist_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, X, rows,
                            d, new_x, dist);
         NNGP_LAUNCH_CHECK();
-        const bool wave_d2 = d2_by_waves(m, d);
+        const bool wave_d2 = d2_by_waves(m, d), pair_d2 = d2_by_pairs(m, d);
+        const bool sel_d2 = !wave_d2 && !pair_d2;
         launch_knn_select(dim3(1), knn_xs_bytes(m, d), st, dist, rows, m, X, Y, d, new_x, idx, (double *)nullptr,
-                          ymT, wave_d2 ? (double *)nullptr : D2, wave_d2 ? (double *)nullptr : kd2,
+                          ymT, sel_d2 ? D2 : (double *)nullptr, sel_d2 ? kd2 : (double *)nullptr,
                           spec ? spec_idx : (const int32_t *)nullptr,
                           spec ? hit_flag : (int32_t *)nullptr, knn_xs_doubles(m, d),
                           spec ? spec2_idx : (const int32_t *)nullptr, spec ? host_flag : (int32_t *)nullptr);
@@ -2084,6 +2145,10 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
         if (wave_d2) {
             hipLaunchKernelGGL(d2_wave_kernel, dim3((unsigned)(m * (m + 1) / 2 + m)), dim3(64), 0, st, X, idx, m,
                                d, new_x, D2, kd2);
+            NNGP_LAUNCH_CHECK();
+        } else if (pair_d2) {
+            hipLaunchKernelGGL(d2_pairs_kernel, dim3((unsigned)((m * (m + 1) / 2 + m + 255) / 256)), dim3(256), 0, st, X,
+                               idx, m, d, new_x, D2, kd2);
             NNGP_LAUNCH_CHECK();
         }
         if (phase == PREDICT_SELECT) return NNGP_OK;
@@ -2159,15 +2224,20 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
     hipLaunchKernelGGL(knn_dist_kernel, dim3((unsigned)((rows + 63) / 64), (unsigned)nq), dim3(64), 0, st, X,
                        rows, d, Q, dist);
     NNGP_LAUNCH_CHECK();
-    const bool wave_d2 = d2_by_waves(m, d);
+    const bool wave_d2 = d2_by_waves(m, d), pair_d2 = d2_by_pairs(m, d);
     launch_knn_select(dim3(1, (unsigned)nq), knn_xs_bytes(m, d), st, dist, rows, m, X, Y, d, Q, idx_out,
-                      (double *)nullptr, ymT, wave_d2 ? (double *)nullptr : D2, (double *)nullptr,
+                      (double *)nullptr, ymT, (wave_d2 || pair_d2) ? (double *)nullptr : D2, (double *)nullptr,
                       (const int32_t *)nullptr, (int32_t *)nullptr, knn_xs_doubles(m, d), (const int32_t *)nullptr,
                       (int32_t *)nullptr);
     NNGP_LAUNCH_CHECK();
     if (wave_d2) {
         hipLaunchKernelGGL(d2_wave_kernel, dim3((unsigned)(m * (m + 1) / 2), (unsigned)nq), dim3(64), 0, st, X,
                            idx_out, m, d, Q, D2, (double *)nullptr);
+        NNGP_LAUNCH_CHECK();
+    }
+    if (pair_d2) {
+        hipLaunchKernelGGL(d2_pairs_kernel, dim3((unsigned)((m * (m + 1) / 2 + 255) / 256), (unsigned)nq), dim3(256), 0,
+                           st, X, idx_out, m, d, Q, D2, (double *)nullptr);
         NNGP_LAUNCH_CHECK();
     }
     // the counters are zeroed (above) before the event the sweep's mean kernels wait behind
