@@ -407,14 +407,25 @@ class Parareal():
             if not hasattr(self, '_preds_scratch') or self._preds_scratch.device != U1.device:
                 self._preds_scratch = torch.empty(self.n, dtype=torch.float64, device=U1.device)
             hits = ctypes.c_int32(0)
+            # auto speculation (-1): after an iteration whose guesses hit fewer than 5 % of its
+            # slices (a chaotic field: TomLab N = 256 hits 1-3 of ~250), the next 7 iterations run
+            # without the speculative batch and re-speculation -- their side-stream fits only
+            # compete with the sweep's own (TomLab 3.54 -> 2.64 s over 20 iterations) -- then it is
+            # tried again.  The fits, hence every iterate, are the same either way.
+            spec = self._run_speculate
+            if spec < 0 and getattr(self, '_spec_skip', 0) > 0:
+                self._spec_skip -= 1
+                spec = 0
             _lib.check(lib.nngp_correction_sweep(
                 ctypes.byref(cs), _lib.TABLEAU[solver.G], solver.step_mode, solver.Ng, t_dev.data_ptr(), I, N,
                 U1.data_ptr(), UG1.data_ptr(), UF.data_ptr(), UG.data_ptr(), _lib.MODEL_NNGP, X.data_ptr(),
                 Y.data_ptr(), int(rows), m, len(jit), jp, model.n_restarts, th0.data_ptr(), float(model.fatol),
-                float(model.xatol), model.maxfev, self._preds_scratch.data_ptr(), self._run_speculate,
+                float(model.xatol), model.maxfev, self._preds_scratch.data_ptr(), spec,
                 ctypes.byref(hits), ctypes.byref(g_ms), stream))
             model.train_count += model.n_fits * (N - I)
             self.spec_hits.append(int(hits.value))
+            if spec < 0 and N - I >= 2 and hits.value < 0.05 * (N - I):
+                self._spec_skip = 7
         elif isinstance(model, GPjax_p):
             Xg, alpha, coef = model._dev
             _lib.check(lib.nngp_correction_sweep(
@@ -566,6 +577,7 @@ class Parareal():
         self.spec_hits = []
         # run(..., speculate=, shard_corrections=) override the constructor's settings for this run
         self._run_speculate = int(kwargs.get('speculate', self.speculate))
+        self._spec_skip = 0   # auto speculation: iterations left to run without it (_correction_sweep)
         self._run_shard = kwargs.get('shard_corrections', self.shard_corrections)
         self._run_native_comm = bool(kwargs.get('native_comm', True))
         tspan, N, epsilon, n = self.tspan, self.N, self.epsilon, self.n

@@ -196,6 +196,23 @@ def test_fused_guess_chain_keeps_hits_and_bits(gpu, case, monkeypatch):
     assert np.array_equal(np.nan_to_num(a['u'], nan=7.0), np.nan_to_num(b['u'], nan=7.0))
 
 
+def test_auto_speculation_pauses_after_a_low_hit_rate(gpu):
+    """speculate=-1 (auto): after an iteration whose guesses hit < 5 % of its slices the next 7
+    iterations run without speculation, then it is tried again (a chaotic field: TomLab); the run
+    is bitwise the unspeculated one."""
+    ode = gpu.ThomasLabyrinth(normalization='-11')
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=10, Nf=3910, F='RK4', G='RK1')
+    p = gpu.Parareal(ode, s, [0, 100], 256, epsilon=5e-7, verbose=None)
+    kw = dict(model='nngp', nn=18, n_restarts=1, fatol=1e-3, xatol=1e-3, seed=45, early_stop=10)
+    a = p.run(speculate=0, **kw)
+    b = p.run(**kw)
+    hits = b['timings']['spec_hits']
+    print('TomLab N=256 auto speculation hits per iteration', hits)
+    assert hits[0] < 0.05 * 255 and hits[1:8] == [0] * 7
+    assert a['k'] == b['k'] and a['conv_int'] == b['conv_int']
+    assert np.array_equal(np.nan_to_num(a['u'], nan=7.0), np.nan_to_num(b['u'], nan=7.0))
+
+
 def test_run_kwargs_override_constructor_settings(gpu):
     """run(..., speculate=...) applies to that run only (the constructor's value otherwise)."""
     ode = gpu.Lorenz(normalization='-11')
