@@ -382,25 +382,37 @@ __device__ __forceinline__ void knn_select_dev(
             kv[j] = r < rows ? dist_key(dist[r]) : 0;
         }
     }
-    // 0) threshold select (K > 0): the m-th smallest high word T of the keys by a 4-pass radix
-    //    select (8-bit digits, LDS histograms), then every row with high word <= T -- a superset
-    //    of the m nearest, usually m plus a few -- is ranked exactly by (key, row) against the
-    //    others.  Bitwise the rounds below (the ordered m smallest pairs are unique); they remain
-    //    the path when more than SEL_CAND rows tie at or below T (duplicated training rows).
+    // 0) threshold select: the m-th smallest high word T of the keys by a 4-pass radix select
+    //    (8-bit digits, LDS histograms), then every row with high word <= T -- a superset of the
+    //    m nearest, usually m plus a few -- is ranked exactly by (key, row) against the others.
+    //    Bitwise the rounds below (the ordered m smallest pairs are unique); they remain the path
+    //    when more than SEL_CAND rows tie at or below T (duplicated training rows).  K > 0: the
+    //    thread's keys from registers; K = 0 (rows > 4 096): re-read from dist (L2-resident) on
+    //    each of the 5 passes -- against the rounds' m passes over all rows (TomLab N = 256 late
+    //    in its run: ~25 000 rows, m = 18, 172 us per select with the rounds alone).
     bool done = false;
-    if constexpr (K > 0) {
+    auto for_keys = [&](auto &&f) {
+        if constexpr (K > 0) {
+#pragma unroll
+            for (int j = 0; j < K; j++)
+                if (kr[j] >= 0) f(kv[j], kr[j]);
+        } else {
+#pragma unroll 8
+            for (int r = tid; r < rows; r += 256) f(dist_key(dist[r]), r);
+        }
+    };
+    {
         uint32_t prefix = 0;
         int need = m;
         for (int pass = 0; pass < 4; pass++) {
             const int shift = 24 - 8 * pass;
             sh.hist[tid] = 0;   // 256 threads = 256 bins
             __syncthreads();
-#pragma unroll
-            for (int j = 0; j < K; j++) {
-                const uint32_t hk = (uint32_t)(kv[j] >> 32);
-                const bool in = kr[j] >= 0 && (pass == 0 || (hk >> (shift + 8)) == (prefix >> (shift + 8)));
+            for_keys([&](uint64_t key, int) {
+                const uint32_t hk = (uint32_t)(key >> 32);
+                const bool in = pass == 0 || (hk >> (shift + 8)) == (prefix >> (shift + 8));
                 if (in) atomicAdd(&sh.hist[(hk >> shift) & 255], 1u);
-            }
+            });
             __syncthreads();
             if (wid == 0) {   // the digit whose bin holds the need-th smallest: lane l scans bins 4l..4l+3
                 const uint32_t h0 = sh.hist[4 * lane], h1 = sh.hist[4 * lane + 1], h2 = sh.hist[4 * lane + 2],
@@ -432,15 +444,15 @@ __device__ __forceinline__ void knn_select_dev(
         }
         if (tid == 0) sh.nc = 0;
         __syncthreads();
-#pragma unroll
-        for (int j = 0; j < K; j++)
-            if (kr[j] >= 0 && (uint32_t)(kv[j] >> 32) <= prefix) {
+        for_keys([&](uint64_t key, int row) {
+            if ((uint32_t)(key >> 32) <= prefix) {
                 const int p = atomicAdd(&sh.nc, 1);
                 if (p < SEL_CAND) {
-                    sh.ck[p] = kv[j];
-                    sh.ci[p] = kr[j];
+                    sh.ck[p] = key;
+                    sh.ci[p] = row;
                 }
             }
+        });
         __syncthreads();
         const int L = sh.nc;
         if (L <= SEL_CAND) {   // uniform

@@ -212,6 +212,27 @@ def test_knn_vs_oracle(gpu, rows, d, m):
     assert np.array_equal(dist.cpu().numpy(), od)
 
 
+@pytest.mark.parametrize('rows,d,m,dups', [(30000, 3, 18, 0), (20000, 3, 64, 0), (9000, 3, 18, 400),
+                                          (4097, 2, 12, 0)])
+def test_knn_streaming_select_vs_oracle(gpu, rows, d, m, dups):
+    """rows > 4 096: the select streams its keys from memory through the radix threshold passes;
+    with `dups` copies of the query's nearest row more than SEL_CAND (256) rows tie at the threshold
+    and the m rounds take over.  Bitwise the oracle either way (ordered by distance, then row)."""
+    import torch
+    rng = np.random.default_rng(rows + d + dups)
+    X = rng.standard_normal((rows, d))
+    q = X[rows // 3] + 1e-3
+    if dups:
+        X[rng.choice(rows, size=dups, replace=False)] = X[rows // 3]
+    idx = torch.empty(m, dtype=torch.int32, device='cuda')
+    dist = torch.empty(m, dtype=torch.float64, device='cuda')
+    Xt, qt = _t(torch, X), _t(torch, q)
+    gpu._lib.check(gpu.lib().nngp_knn(Xt.data_ptr(), rows, d, qt.data_ptr(), m, idx.data_ptr(), dist.data_ptr(), None))
+    oi, od = O.knn(X, q, m)
+    assert np.array_equal(idx.cpu().numpy(), oi)
+    assert np.array_equal(dist.cpu().numpy(), od)
+
+
 def _nm_case(m, d, seed):
     rng = np.random.default_rng(seed)
     base = rng.uniform(-0.5, 0.5, size=d)
