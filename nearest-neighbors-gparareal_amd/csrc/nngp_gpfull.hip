@@ -255,6 +255,82 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 static constexpr int GPF_TM = 64;              // update tile
 static constexpr int GPF_US = GPB + 2;         // LDS row stride of the staged panel rows
 
+template <bool FULL>
+__device__ __forceinline__ void gpf_update_tile(double *__restrict__ Ab, int ld, int n, int p0, int pb, int i0,
+                                                int j0, bool diag, double *Li, double *Lj) {
+    const int tid = threadIdx.x;
+    const int w = tid >> 6, lane = tid & 63;
+    const int kq = lane >> 4, ra = 16 * w + (lane & 15);
+    const int ncb = FULL ? 4 : (diag ? w + 1 : 4);   // column blocks at or left of the diagonal
+    // this lane's 16 elements of A: rows i0 + 16w + kq + 4r, columns j0 + 16cb + (lane & 15)
+    double *arow = Ab + (size_t)(i0 + 16 * w + kq) * ld + j0 + (lane & 15);
+    double old[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+#pragma unroll
+        for (int cb = 0; cb < 4; cb++) {
+            if constexpr (FULL) {
+                old[cb][r] = arow[(size_t)(4 * r) * ld + 16 * cb];
+            } else {
+                const int i = i0 + 16 * w + kq + 4 * r, j = j0 + 16 * cb + (lane & 15);
+                old[cb][r] = (cb < ncb && i <= n && j < n && j <= i) ? Ab[(size_t)i * ld + j] : 0.0;
+            }
+        }
+    }
+    constexpr int SU = GPF_TM * GPB / 256;   // consecutive lanes: consecutive k of a row
+    double vi[SU], vj[SU];
+    if constexpr (FULL) {   // thread: rows tid/32 + 8u, column tid%32 of the panel
+        const double *pi = Ab + (size_t)(i0 + (tid >> 5)) * ld + p0 + (tid & 31);
+        const double *pj = Ab + (size_t)(j0 + (tid >> 5)) * ld + p0 + (tid & 31);
+#pragma unroll
+        for (int u = 0; u < SU; u++) {
+            vi[u] = pi[(size_t)(8 * u) * ld];
+            vj[u] = pj[(size_t)(8 * u) * ld];
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < SU; u++) {
+            const int t = tid + 256 * u, rr = t / GPB, k = t % GPB;
+            vi[u] = (i0 + rr <= n && k < pb) ? Ab[(size_t)(i0 + rr) * ld + p0 + k] : 0.0;
+            vj[u] = (j0 + rr < n && k < pb) ? Ab[(size_t)(j0 + rr) * ld + p0 + k] : 0.0;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+        const int t = tid + 256 * u, rr = t / GPB, k = t % GPB;
+        Li[rr * GPF_US + k] = vi[u];
+        Lj[rr * GPF_US + k] = vj[u];
+    }
+    __syncthreads();
+    const int kend = FULL ? GPB : (pb + 3) & ~3;   // the zero padding past pb adds exact zeros
+    f64x4 acc[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; cb++) acc[cb] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < GPB; k += 4) {
+        if (k >= kend) break;
+        const double av = Li[ra * GPF_US + k + kq];
+#pragma unroll
+        for (int cb = 0; cb < 4; cb++)
+            if (cb < ncb)
+                acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Lj[(16 * cb + (lane & 15)) * GPF_US + k + kq],
+                                                               acc[cb], 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+#pragma unroll
+        for (int cb = 0; cb < 4; cb++) {
+            if constexpr (FULL) {
+                arow[(size_t)(4 * r) * ld + 16 * cb] = old[cb][r] - acc[cb][r];
+            } else {
+                if (cb >= ncb) continue;
+                const int i = i0 + 16 * w + kq + 4 * r, j = j0 + 16 * cb + (lane & 15);
+                if (i <= n && j < n && j <= i) Ab[(size_t)i * ld + j] = old[cb][r] - acc[cb][r];
+            }
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256, 3) gpf_update_kernel(double *__restrict__ A, int n, int p0, int pb,
                                                              const int32_t *__restrict__ fail,
                                                              const double *__restrict__ Lpan, int ntiles, int nmat) {
@@ -279,60 +355,15 @@ __global__ void __launch_bounds__(256, 3) gpf_update_kernel(double *__restrict__
     const int tj = tile - ti * (ti + 1) / 2;
     const int q0 = p0 + pb;
     const int i0 = q0 + ti * GPF_TM, j0 = q0 + tj * GPF_TM;
+    // an off-diagonal tile inside the matrix with a full panel (most of them): no guards, and
+    // row pointers with the column blocks as immediate offsets (the guarded form spent ~1 000
+    // VALU per wave on index arithmetic, issue-stalling 39 % of its cycles beside 27 % active,
+    // profiles/r04/pmc_gpf_update_r4af.txt)
     __shared__ double Li[GPF_TM * GPF_US], Lj[GPF_TM * GPF_US];
-    const int tid = threadIdx.x;
-    const int w = tid >> 6, lane = tid & 63;
-    const int kq = lane >> 4, ra = 16 * w + (lane & 15);
-    const int ncb = (ti == tj) ? w + 1 : 4;      // column blocks at or left of the diagonal
-    double old[4][4];
-#pragma unroll
-    for (int cb = 0; cb < 4; cb++) {
-        const int j = j0 + 16 * cb + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int i = i0 + 16 * w + kq + 4 * r;
-            old[cb][r] = (cb < ncb && i <= n && j < n && j <= i) ? Ab[(size_t)i * ld + j] : 0.0;
-        }
-    }
-    constexpr int SU = GPF_TM * GPB / 256;   // consecutive lanes: consecutive k of a row
-    double vi[SU], vj[SU];
-#pragma unroll
-    for (int u = 0; u < SU; u++) {
-        const int t = tid + 256 * u, rr = t / GPB, k = t % GPB;
-        vi[u] = (i0 + rr <= n && k < pb) ? Ab[(size_t)(i0 + rr) * ld + p0 + k] : 0.0;
-        vj[u] = (j0 + rr < n && k < pb) ? Ab[(size_t)(j0 + rr) * ld + p0 + k] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < SU; u++) {
-        const int t = tid + 256 * u, rr = t / GPB, k = t % GPB;
-        Li[rr * GPF_US + k] = vi[u];
-        Lj[rr * GPF_US + k] = vj[u];
-    }
-    __syncthreads();
-    const int kend = (pb + 3) & ~3;              // the zero padding past pb adds exact zeros
-    f64x4 acc[4];
-#pragma unroll
-    for (int cb = 0; cb < 4; cb++) acc[cb] = f64x4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int k = 0; k < GPB; k += 4) {
-        if (k >= kend) break;
-        const double av = Li[ra * GPF_US + k + kq];
-#pragma unroll
-        for (int cb = 0; cb < 4; cb++)
-            if (cb < ncb)
-                acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Lj[(16 * cb + (lane & 15)) * GPF_US + k + kq],
-                                                               acc[cb], 0, 0, 0);
-    }
-#pragma unroll
-    for (int cb = 0; cb < 4; cb++) {
-        if (cb >= ncb) continue;
-        const int j = j0 + 16 * cb + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int i = i0 + 16 * w + kq + 4 * r;
-            if (i <= n && j < n && j <= i) Ab[(size_t)i * ld + j] = old[cb][r] - acc[cb][r];
-        }
-    }
+    if (ti != tj && i0 + GPF_TM - 1 <= n && j0 + GPF_TM <= n && pb == GPB)
+        gpf_update_tile<true>(Ab, ld, n, p0, pb, i0, j0, false, Li, Lj);
+    else
+        gpf_update_tile<false>(Ab, ld, n, p0, pb, i0, j0, ti == tj, Li, Lj);
 }
 
 __device__ __forceinline__ double block_sum(double v, double *red) {
