@@ -73,26 +73,32 @@ __global__ void gpf_d2_kernel(const double *__restrict__ X, int n, int d, double
 
 // lower triangle (incl. diagonal) of K for point b: sigma_y^2 * exp(c * D2) (+ 10^jitter on the
 // diagonal), kernel_np's order (models.py:302-304) and K + eye*10**jitter (:308); row n = y^T
-__global__ void gpf_build_kernel(const double *__restrict__ D2, int n, const double *__restrict__ Y, int d,
-                                 const GPPoint *__restrict__ pts, double *__restrict__ A,
-                                 const int32_t *__restrict__ fail) {
+// Workgroup = GPF_BROWS consecutive rows of one matrix (blockIdx.y), its threads over each row's
+// lower-triangle columns j <= i only (a grid-stride loop over all n^2 entries left half of its
+// threads on the upper triangle and divided by n per entry); the block past the last row writes y.
+static constexpr int GPF_BROWS = 8;
+__global__ void __launch_bounds__(256) gpf_build_kernel(const double *__restrict__ D2, int n,
+                                                        const double *__restrict__ Y, int d,
+                                                        const GPPoint *__restrict__ pts, double *__restrict__ A,
+                                                        const int32_t *__restrict__ fail) {
     const int b = blockIdx.y;
     if (fail[b]) return;
     const GPPoint p = pts[b];
     const int ld = n + 1;
     double *Ab = A + (size_t)b * ld * ld;
-    const size_t nn = (size_t)n * n;
-    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < nn + n; t += (size_t)gridDim.x * blockDim.x) {
-        if (t >= nn) {   // row n: the training column
-            const int j = (int)(t - nn);
-            Ab[(size_t)n * ld + j] = Y[(size_t)j * d + p.coord];
-            continue;
+    const int r0 = blockIdx.x * GPF_BROWS;
+    if (r0 >= n) {   // row n: the training column
+        for (int j = threadIdx.x; j < n; j += 256) Ab[(size_t)n * ld + j] = Y[(size_t)j * d + p.coord];
+        return;
+    }
+    for (int i = r0; i < min(r0 + GPF_BROWS, n); i++) {
+        const double *drow = D2 + (size_t)i * n;
+        double *arow = Ab + (size_t)i * ld;
+        for (int j = threadIdx.x; j <= i; j += 256) {
+            double v = p.psy * exp(p.c * drow[j]);
+            if (i == j) v = v + p.jp;
+            arow[j] = v;
         }
-        const int i = (int)(t / n), j = (int)(t - (size_t)i * n);
-        if (j > i) continue;
-        double v = p.psy * exp(p.c * D2[t]);
-        if (i == j) v = v + p.jp;
-        Ab[(size_t)i * ld + j] = v;
     }
 }
 
@@ -487,8 +493,7 @@ int gpfull_mean(const double *X, int64_t rows, int d, const double *q, const dou
 static int gpf_eval(const double *D2, int n, const double *Y, int d, const GPPoint *pts, int nb, double *A,
                     int32_t *fail, double *fval, double *alpha_out, double *Lpan, hipStream_t st) {
     NNGP_HIP_CHECK(hipMemsetAsync(fail, 0, sizeof(int32_t) * nb, st));
-    const size_t cnt = (size_t)n * n + n;
-    const unsigned bx = (unsigned)std::min<size_t>((cnt + 255) / 256, 1024);
+    const unsigned bx = (unsigned)((n + GPF_BROWS - 1) / GPF_BROWS + 1);   // + the y row's block
     hipLaunchKernelGGL(gpf_build_kernel, dim3(bx, nb), dim3(256), 0, st, D2, n, Y, d, pts, A, fail);
     NNGP_LAUNCH_CHECK();
     for (int p0 = 0; p0 < n; p0 += GPB) {
