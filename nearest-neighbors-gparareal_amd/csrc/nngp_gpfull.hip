@@ -12,8 +12,8 @@
 // factorisations of the (n+1) x (n+1) matrix [K; y^T] (row n rides along as a "row below", so the
 // factor's last row is z = L^-1 y and y.alpha = z.z):
 //   gpf_build_kernel   K of every point of the batch (lower triangle) from the hoisted D^2, + y^T
-//   gpf_diag_kernel    blocked right-looking Cholesky, panel j: one wave per matrix factors the
-//                      32x32 diagonal block in registers (dpotf2 order)
+//   gpf_diag_kernel    blocked right-looking Cholesky, panel j: one wave per two matrices factors
+//                      their 32x32 diagonal blocks in registers (dpotf2 order)
 //   gpf_rows_kernel    each thread solves one row below the diagonal block
 //   gpf_update_kernel  trailing update A22 -= L21 L21^T, 64x64 lower tiles, LDS-staged panels, on
 //                      the FP64 matrix cores (v_mfma_f64_16x16x4_f64)
@@ -108,29 +108,34 @@ __device__ __forceinline__ double lane_double(double v, int lane) {   // v of la
     return __hiloint2double(hi, lo);
 }
 
-// Right-looking Cholesky of the pb x pb diagonal block held by one wave: lane i < pb owns row i
-// in a[0..GPB) (lower part meaningful).  Column j (dpotf2's order): L_jj = sqrt(a_jj), L_ij =
-// a_ij * (1/L_jj), then a_ik -= L_ij L_kj for j < k <= i.  The column goes through LDS (col[]:
-// one write per lane, then every lane reads the whole column -- broadcast reads issued together)
-// and the updates are selects, not branches.  rinv[j] = 1/L_jj.  False (uniformly) on a pivot
-// that is not > 0 or NaN (LAPACK's info > 0).
-__device__ __forceinline__ bool diag_factor(double (&a)[GPB], double (&rinv)[GPB], int i, int pb, double *col) {
+// Right-looking Cholesky of the pb x pb diagonal blocks of TWO matrices held by one wave: lane
+// 32h + i owns row i of matrix h in a[0..GPB) (lower part meaningful).  Column j (dpotf2's
+// order): L_jj = sqrt(a_jj), L_ij = a_ij * (1/L_jj), then a_ik -= L_ij L_kj for j < k <= i.  The
+// column goes through LDS (col[32h + i]: one write per lane, then every lane reads its half's
+// column -- broadcast reads issued together) and the updates are selects, not branches.
+// rinv[j] = 1/L_jj.  bad: this half met a pivot that is not > 0 or NaN (LAPACK's info > 0); its
+// later columns then compute garbage that nobody reads.  (One matrix per wave left lanes 32-63
+// idle and put 1 152 matrices on 1 024 SIMDs, two waves on some: the launch took two waves' time.)
+__device__ __forceinline__ void diag_factor(double (&a)[GPB], double (&rinv)[GPB], int i, int h, int pb,
+                                            double *col, bool &bad) {
+    bad = false;
 #pragma unroll
     for (int j = 0; j < GPB; j++) {
         rinv[j] = 1.0;
         if (j < pb) {
-            const double djj = lane_double(a[j], j);
-            if (!(djj > 0.0)) return false;
+            const double d0 = lane_double(a[j], j), d1 = lane_double(a[j], 32 + j);
+            const double djj = h ? d1 : d0;
+            bad = bad || !(djj > 0.0);
             const double ljj = sqrt(djj);
             const double rj = 1.0 / ljj;
             rinv[j] = rj;
             const double lij = a[j] * rj;
             a[j] = (i == j) ? ljj : ((i > j) ? lij : a[j]);
-            if (i < GPB) col[i] = a[j];
+            col[32 * h + i] = a[j];
             wave_sync_lds();
             double lk[GPB];
 #pragma unroll
-            for (int k = j + 1; k < GPB; k++) lk[k] = col[k];
+            for (int k = j + 1; k < GPB; k++) lk[k] = col[32 * h + k];
 #pragma unroll
             for (int k = j + 1; k < GPB; k++) {
                 const double upd = a[k] - a[j] * lk[k];
@@ -139,11 +144,10 @@ __device__ __forceinline__ bool diag_factor(double (&a)[GPB], double (&rinv)[GPB
             wave_sync_lds();
         }
     }
-    return true;
 }
 
 // Panel p0 (width pb), in two launches.
-// gpf_diag_kernel: ONE wave per matrix factors the diagonal block in registers (diag_factor) and
+// gpf_diag_kernel: one wave per TWO matrices factors their diagonal blocks in registers (diag_factor) and
 // leaves L11 and 1/L_jj in Lpan[b] = [L11 (GPB x GPB, lower) | rinv (GPB)]; fail[b] on a failed
 // pivot.  (Round 3 factored it in every row-solve workgroup of the matrix, and the factor's ~190
 // VGPRs held the whole row-solve launch at two waves per SIMD: 118 us per panel at n = 753 with
@@ -156,27 +160,27 @@ __device__ __forceinline__ bool diag_factor(double (&a)[GPB], double (&rinv)[GPB
 // block.
 static constexpr int LPS = GPB * GPB + GPB;   // Lpan doubles per matrix
 
-__global__ void __launch_bounds__(64) gpf_diag_kernel(const double *__restrict__ A, int n, int p0, int pb,
+__global__ void __launch_bounds__(64) gpf_diag_kernel(const double *__restrict__ A, int n, int p0, int pb, int nmat,
                                                        int32_t *__restrict__ fail, double *__restrict__ Lpan) {
-    const int b = blockIdx.x;
-    if (fail[b]) return;
+    const int h = threadIdx.x >> 5, i = threadIdx.x & 31;
+    const int b = 2 * blockIdx.x + h;
+    const bool act = b < nmat && !fail[b];   // half-uniform; an idle half runs along on zeros
     const int ld = n + 1;
-    const double *Ab = A + (size_t)b * ld * ld;
-    __shared__ double col[GPB];
-    const int i = threadIdx.x;
+    const double *Ab = A + (size_t)(act ? b : 0) * ld * ld;
+    __shared__ double col[2 * GPB];
     double a[GPB], rv[GPB];
 #pragma unroll
-    for (int k = 0; k < GPB; k++) a[k] = (i < pb && k <= i) ? Ab[(size_t)(p0 + i) * ld + p0 + k] : 0.0;
-    const bool ok = diag_factor(a, rv, i, pb, col);
-    if (!ok) {
+    for (int k = 0; k < GPB; k++) a[k] = (act && i < pb && k <= i) ? Ab[(size_t)(p0 + i) * ld + p0 + k] : 0.0;
+    bool bad;
+    diag_factor(a, rv, i, h, pb, col, bad);
+    if (!act) return;
+    if (bad) {
         if (i == 0) fail[b] = 1;
         return;
     }
     double *Lb = Lpan + (size_t)b * LPS;
-    if (i < GPB) {
 #pragma unroll
-        for (int k = 0; k < GPB; k++) Lb[i * GPB + k] = (i < pb && k <= i) ? a[k] : 0.0;
-    }
+    for (int k = 0; k < GPB; k++) Lb[i * GPB + k] = (i < pb && k <= i) ? a[k] : 0.0;
     if (i == 0) {
 #pragma unroll
         for (int k = 0; k < GPB; k++) Lb[GPB * GPB + k] = rv[k];
@@ -500,7 +504,7 @@ static int gpf_eval(const double *D2, int n, const double *Y, int d, const GPPoi
         const int pb = std::min(GPB, n - p0);
         const int below = n + 1 - p0 - pb;   // includes row n (y)
         const unsigned chunks = (unsigned)std::max(1, (below + 63) / 64);
-        hipLaunchKernelGGL(gpf_diag_kernel, dim3(nb), dim3(64), 0, st, A, n, p0, pb, fail, Lpan);
+        hipLaunchKernelGGL(gpf_diag_kernel, dim3((nb + 1) / 2), dim3(64), 0, st, A, n, p0, pb, nb, fail, Lpan);
         if (pb == GPB)
             hipLaunchKernelGGL(gpf_rows_kernel<true>, dim3(chunks, nb), dim3(64), 0, st, A, n, p0, pb, fail, Lpan);
         else

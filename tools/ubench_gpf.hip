@@ -18,16 +18,17 @@ void comm_release() {}
 using namespace nngp;
 
 __global__ void __launch_bounds__(64) diag_loop(const double *A, int reps, double *out, long long *cyc) {
-    __shared__ double col[GPB];
+    __shared__ double col[2 * GPB];
     const int i = threadIdx.x;
     double a[GPB], rv[GPB];
-    for (int k = 0; k < GPB; k++) a[k] = (k <= i && i < GPB) ? A[i * GPB + k] : 0.0;
+    for (int k = 0; k < GPB; k++) a[k] = (k <= (i & 31)) ? A[(i & 31) * GPB + k] : 0.0;
     double acc = 0.0;
     long long t0 = clock64();
     for (int r = 0; r < reps; r++) {
         double b[GPB];
         for (int k = 0; k < GPB; k++) b[k] = a[k] + acc * 1e-300;
-        diag_factor(b, rv, i, GPB, col);
+        bool bad;
+        diag_factor(b, rv, i & 31, i >> 5, GPB, col, bad);
         acc += b[GPB - 1] + rv[3];
     }
     long long t1 = clock64();
@@ -88,7 +89,7 @@ int main() {
     const int reps = 50;
     hipLaunchKernelGGL(diag_loop, dim3(1), dim3(64), 0, 0, dA, reps, dout, dc);
     hipMemcpy(&cyc, dc, sizeof(cyc), hipMemcpyDeviceToHost);
-    printf("diag_factor 32x32 (one wave): %.0f cycles\n", (double)cyc / reps);
+    printf("diag_factor 2 x 32x32 (one wave): %.0f cycles\n", (double)cyc / reps);
     hipLaunchKernelGGL(rowsolve_loop, dim3(1), dim3(256), 0, 0, dL, reps, dout, dc);
     hipMemcpy(&cyc, dc, sizeof(cyc), hipMemcpyDeviceToHost);
     printf("row solve 32 columns (256 threads): %.0f cycles\n", (double)cyc / reps);
@@ -126,7 +127,7 @@ int main() {
         hipEventRecord(e0, 0);
         for (int r = 0; r < 10; r++) {
             const int below = n + 1 - GPB;
-            hipLaunchKernelGGL(gpf_diag_kernel, dim3(nb), dim3(64), 0, 0, w.A, n, 0, GPB, w.fail, w.Lpan);
+            hipLaunchKernelGGL(gpf_diag_kernel, dim3((nb + 1) / 2), dim3(64), 0, 0, w.A, n, 0, GPB, nb, w.fail, w.Lpan);
             hipLaunchKernelGGL(gpf_rows_kernel<true>, dim3((below + 63) / 64, nb), dim3(64), 0, 0, w.A, n, 0, GPB,
                                w.fail, w.Lpan);
         }
