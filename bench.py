@@ -116,9 +116,8 @@ def fine_sweep_bench(torch, g, world, rank, steps, warmup, steps_per_slice, slic
     out = torch.empty_like(u0)
     gathered = torch.empty((n_total, 3), dtype=torch.float64, device='cuda')
     ev = []
-    # the all-gather of the end states: the library's RCCL communicator (include/nngp.h
-    # nngp_allgather_states), torch.distributed's if it cannot be created
-    native = world > 1 and g._lib.comm_for(None)
+    # the all-gather of the end states: torch.distributed's (RCCL); the library's own communicator
+    # (include/nngp.h nngp_allgather_states) is checked against it after the timed region
     st = torch.cuda.current_stream().cuda_stream
 
     def one(record):
@@ -130,9 +129,7 @@ def fine_sweep_bench(torch, g, world, rank, steps, warmup, steps_per_slice, slic
         if record:
             b.record()
             ev.append((a, b))
-        if native:
-            g._lib.check(g.lib().nngp_allgather_states(out.data_ptr(), gathered.data_ptr(), out.numel(), st))
-        elif world > 1:
+        if world > 1:
             torch.distributed.all_gather_into_tensor(gathered, out)
 
     for _ in range(warmup):
@@ -148,8 +145,21 @@ def fine_sweep_bench(torch, g, world, rank, steps, warmup, steps_per_slice, slic
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(tt.item())
     kernel_s = np.mean([a.elapsed_time(b) / 1e3 for a, b in ev])
-    return elapsed, kernel_s, n_total, out, ('nngp_allgather_states' if native else
-                                             ('torch all_gather_into_tensor' if world > 1 else None))
+    check = None
+    if world > 1:   # the library's RCCL all-gather on the same end states, bitwise torch's
+        try:
+            if g._lib.comm_for(None):
+                native = torch.full_like(gathered, float('nan'))
+                g._lib.check(g.lib().nngp_allgather_states(out.data_ptr(), native.data_ptr(), out.numel(), st))
+                torch.cuda.synchronize()
+                same = torch.tensor([1 if torch.equal(native, gathered) else 0], dtype=torch.int32, device='cuda')
+                torch.distributed.all_reduce(same, op=torch.distributed.ReduceOp.MIN)
+                check = {'nngp_allgather_states_bitwise_torch': bool(same.item())}
+            else:
+                check = {'nngp_allgather_states_bitwise_torch': None, 'note': 'library communicator unavailable'}
+        except Exception as e:   # a report, never fatal to the headline
+            check = {'nngp_allgather_states_bitwise_torch': None, 'error': str(e)[:200]}
+    return elapsed, kernel_s, n_total, out, ('torch all_gather_into_tensor' if world > 1 else None), check
 
 
 def corrections_bench(torch, g, m=15, R=2, n_slices=128):
@@ -777,10 +787,19 @@ def sharded_sweep_timing(torch, g, solver, td, Ufull, Xd, Yd, rows, mdl, world, 
                 400, scratch.data_ptr(), 0, None, None, st))
 
     out = {}
+    finals = {}
     for name, fn in (('python_loop', python_loop), ('native', native)):
         fn()
         out[f'{name}_ms_per_slice'] = timed(fn, 2) / n_sw * 1e3
+        torch.cuda.synchronize()
+        finals[name] = U1.clone()
     out['host_overhead_ms_per_slice_removed'] = out['python_loop_ms_per_slice'] - out['native_ms_per_slice']
+    # the two paths compute the same sweep from the same U1[0]: bitwise equal on every rank
+    same = torch.tensor([1 if torch.equal(finals['python_loop'], finals['native']) else 0], dtype=torch.int32,
+                        device='cuda')
+    if world > 1:
+        torch.distributed.all_reduce(same, op=torch.distributed.ReduceOp.MIN)
+    out['native_bitwise_python_loop'] = bool(same.item())
     out['native_path'] = ('nngp_correction_sweep_sharded (library RCCL communicator)' if comm
                           else 'nngp_correction_sweep (one rank)')
     out['slices'] = n_sw
@@ -858,8 +877,8 @@ def main():
     import nngp_amd as g
     g.lib()
 
-    elapsed, kernel_s, n_total, _, gather_path = fine_sweep_bench(torch, g, world, rank, args.steps, args.warmup,
-                                                     args.steps_per_slice, args.slices_per_gpu)
+    elapsed, kernel_s, n_total, _, gather_path, native_check = fine_sweep_bench(
+        torch, g, world, rank, args.steps, args.warmup, args.steps_per_slice, args.slices_per_gpu)
     total_steps = n_total * args.steps_per_slice * args.steps
     value = total_steps / elapsed
     flops_launch = FLOPS_PER_STEP[('hopf', 'RK4')] * args.steps_per_slice * args.slices_per_gpu
@@ -874,7 +893,7 @@ def main():
         'config': {'workload': 'nonautonomous Hopf (Hopf.py), RK4 fine sweep, 13.6e6 steps/slice',
                    'slices_per_gpu': args.slices_per_gpu, 'total_slices': n_total,
                    'steps_per_slice': args.steps_per_slice, 'parallelism': f'time-slices x{world}',
-                   'allgather': gather_path},
+                   'allgather': gather_path, 'native_allgather_check': native_check},
         'roofline': {'bound': 'fp64-valu', 'achieved': achieved_tf, 'peak': FP64_PEAK_TFLOPS,
                      'unit': 'TFLOP/s', 'frac': achieved_tf / FP64_PEAK_TFLOPS, 'traffic': traffic,
                      **({k: v for k, v in tr.items() if k != 'traffic'} if tr else {}), 'traffic_source': tr_src,

@@ -236,7 +236,10 @@ int64_t nngp_sweep_late_reruns(void);
 int nngp_shutdown(void);
 
 /* ---- 4. full-data GParareal (models.GPjax_p, models.py:273-473) ------------------------------
- * The training set X, Y: DEVICE [rows][d], rows <= 7936.  K = sigma_y^2 exp(-0.5/sigma_x^2 D^2)
+ * The training set X, Y: DEVICE [rows][d], rows >= 1 (no fixed limit: the scratch is rows^2
+ * doubles for D^2 plus (rows+1)^2 per point factored together, batched to <= 8 GB but at least one
+ * point, so device memory bounds rows, ~1e5 on a 288 GB MI355X; up to 7 936 rows the alpha solve
+ * keeps its vector in LDS, past that in its output row).  K = sigma_y^2 exp(-0.5/sigma_x^2 D^2)
  * + 10^jitter I over ALL rows (kernel_np / _fit_gp_np, models.py:300-312), theta = (sigma_x,
  * sigma_y) in linear units.  Points and fits are batched: one blocked Cholesky per point.
  *
@@ -292,7 +295,10 @@ int nngp_allgather_states(const double *send, double *recv, size_t per_rank_elem
  * coordinates (nngp_predict_range), one in-place all-gather of the predictions, and
  * U1[i+1] = preds + UG1[i+1] -- all on `stream`, no host synchronisation.  Bitwise the unsharded
  * sweep on every rank (same inputs, same theta0 draws).  gather: DEVICE [nranks*chunk] scratch.
- * No speculation (every rank would need the whole batch).                                       */
+ * No speculation (every rank would need the whole batch).
+ * Check mode: with a ONE-rank communicator and NNGP_SHARD_EMULATE_RANKS=W in the environment, the
+ * process plays the W ranks of the split in turn (each rank's coordinates into its gather block,
+ * no collective); gather must then hold W*ceil(d/W) doubles.                                     */
 int nngp_correction_sweep_sharded(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps,
                                   const double *t, int I, int N, double *U1, double *UG1, const double *X,
                                   const double *Y, int64_t rows, int m, int n_jitter,

@@ -158,7 +158,14 @@ def sweep_late_reruns():
 
 
 COMM_UID_BYTES = 128
-_comm_key = None
+_comm_state = {'group': None, 'key': None}
+
+
+def comm_release():
+    """Release the library's communicator (nngp_comm_destroy) and forget which group it served."""
+    _comm_state.update(group=None, key=None)
+    if _lib is not None:
+        _lib.nngp_comm_destroy()
 
 
 def comm_for(group=None):
@@ -166,25 +173,43 @@ def comm_for(group=None):
     `group`, created once per group: rank 0 makes the unique id, torch broadcasts it, every rank
     joins on its current device.  Returns True when the native collectives are live for `group`;
     False for a gloo group (ranks sharing one GPU: RCCL refuses duplicate devices) or when RCCL
-    cannot be loaded -- the caller then keeps torch.distributed's collectives."""
-    global _comm_key
+    cannot be loaded on some rank -- the caller then keeps torch.distributed's collectives.
+
+    The ranks agree before the collective init (every rank must be able to resolve RCCL) and after
+    it (every rank's init succeeded), so one failing rank never leaves the others blocked in RCCL.
+    The cache holds the group object itself (its id() cannot be re-used while it is held) and is
+    re-checked against nngp_comm_size, so a communicator released by nngp_shutdown /
+    nngp_comm_destroy is created again."""
+    import torch
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_backend(group) != 'nccl':
         return False
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    key = (id(group), world, rank)
-    if _comm_key == key:
-        return True
+    gobj = group if group is not None else dist.group.WORLD
+    key = (id(gobj), world, rank)
     L = lib()
+    if _comm_state['key'] == key and _comm_state['group'] is gobj:
+        nr, rk = ctypes.c_int(0), ctypes.c_int(-1)
+        L.nngp_comm_size(ctypes.byref(nr), ctypes.byref(rk))
+        if (nr.value, rk.value) == (world, rank):
+            return True
+    _comm_state.update(group=None, key=None)
+
+    def agree(ok):   # MIN over the group's ranks
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device='cuda')
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        return int(flag.item()) == 1
+
     uid = ctypes.create_string_buffer(COMM_UID_BYTES)
-    ok = [True]
-    if rank == 0:
-        ok[0] = L.nngp_comm_unique_id(uid) == 0
-    obj = [(ok[0], uid.raw)]
+    ok = L.nngp_comm_unique_id(uid) == 0   # every rank: resolves RCCL; rank 0's id is the one used
+    if not agree(ok):
+        return False
+    obj = [uid.raw]
     src = 0 if group is None else dist.get_global_rank(group, 0)
     dist.broadcast_object_list(obj, src=src, group=group)
-    if not obj[0][0]:
+    rc = L.nngp_comm_init(world, rank, obj[0])
+    if not agree(rc == 0):
+        L.nngp_comm_destroy()
         return False
-    check(L.nngp_comm_init(world, rank, obj[0][1]))
-    _comm_key = key
+    _comm_state.update(group=gobj, key=key)
     return True

@@ -182,8 +182,13 @@ extern "C" int nngp_correction_sweep_sharded(const nngp_system *sys, int g_table
     }
     NNGP_REQUIRE(nranks >= 1, "no communicator: call nngp_comm_init first");
     const int d = sys->d;
-    const int chunk = (d + nranks - 1) / nranks;   // parareal.shard_bounds(0, d, nranks, rank)
-    const int c0 = std::min(rank * chunk, d), c1 = std::min((rank + 1) * chunk, d);
+    // NNGP_SHARD_EMULATE_RANKS=W on a one-rank communicator: this process plays all W ranks of the
+    // coordinate split in turn -- each rank's [c0, c1) into its own gather block, no collective --
+    // so the split, the partial last block and the block placement are checked on one GPU against
+    // the unsharded sweep (tests/test_gpu_distributed.py).  The caller sizes gather to W * chunk.
+    const int vranks = nranks == 1 ? std::max(1, env_int("NNGP_SHARD_EMULATE_RANKS", 1)) : nranks;
+    const int chunk = (d + vranks - 1) / vranks;   // parareal.shard_bounds(0, d, vranks, rank)
+    const int r_lo = nranks == 1 ? 0 : rank, r_hi = nranks == 1 ? vranks : rank + 1;
     const int64_t n_fits = (int64_t)d * n_jitter * n_restarts;
     hipStream_t st = (hipStream_t)stream;
     int err = 0;
@@ -208,13 +213,19 @@ extern "C" int nngp_correction_sweep_sharded(const nngp_system *sys, int g_table
         rc = nngp_rk_batch(sys, g_tableau, g_step_mode, 1, t + i, t + i + 1, g_steps, ui, ug_next, stream);
         if (rc) break;
         if (ev) NNGP_HIP_CHECK(hipEventRecord(ev[2 * j + 1], st));
-        if (c1 > c0)
-            rc = predict_impl(X, Y, rows, d, ui, m, n_jitter, jitter_exp_host, n_restarts, theta0 + j * n_fits * 2,
-                              fatol, xatol, maxfev, gather + (size_t)rank * chunk, nullptr, nullptr, nullptr,
-                              nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, st, c0, c1, nullptr, nullptr);
+        for (int r = r_lo; r < r_hi && rc == NNGP_OK; r++) {
+            const int c0 = std::min(r * chunk, d), c1 = std::min((r + 1) * chunk, d);
+            if (c1 > c0)
+                rc = predict_impl(X, Y, rows, d, ui, m, n_jitter, jitter_exp_host, n_restarts,
+                                  theta0 + j * n_fits * 2, fatol, xatol, maxfev, gather + (size_t)r * chunk, nullptr,
+                                  nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, st, c0, c1,
+                                  nullptr, nullptr);
+        }
         if (rc) break;
-        rc = comm_allgather(gather + (size_t)rank * chunk, gather, (size_t)chunk, st);
-        if (rc) break;
+        if (nranks > 1) {   // in place: this rank's block sits at rank * chunk of the gather buffer
+            rc = comm_allgather(gather + (size_t)rank * chunk, gather, (size_t)chunk, st);
+            if (rc) break;
+        }
         rc = nngp_parareal_update(d, gather, zeros, ug_next, U1 + (size_t)(i + 1) * d, stream);
     }
     if (ev && rc == NNGP_OK) {   // sum the G launches once the sweep has drained

@@ -1592,6 +1592,9 @@ __device__ __forceinline__ bool chain_barrier(uint32_t *bar, uint32_t &target, i
             }
             __builtin_amdgcn_s_sleep(1);
         }
+        // a workgroup arriving after the others gave up finds bar >= target at once: it must not
+        // run the next phase on data the others never finished writing
+        if (__hip_atomic_load(berr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) s_bad = 1;
         __threadfence();
     }
     __syncthreads();
@@ -2483,7 +2486,11 @@ int chain_sweep(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t 
     const bool prof = env_int("NNGP_CHAIN_PROF", 0) != 0;
     c.prof = prof ? (uint64_t *)(res->stop + 4) : nullptr;
     c.berr = res->stop + 28;   // byte 112 of the 128-byte host-mapped block (prof: bytes 16..87)
-    c.bar_ticks = (uint64_t)(2.0e6 * res->tick_khz / 1e3);   // 2 s
+    // the grid-barrier timeout: other workgroups wait at barrier 1 while block 0 integrates G, so
+    // it scales with the coarse step count (4 us per step covers every G kernel here, RK8 Burgers
+    // ~1.4 us) and is never below NNGP_CHAIN_BARRIER_US (default 2 s)
+    const double bar_us = std::max((double)std::max(0, env_int("NNGP_CHAIN_BARRIER_US", 2000000)), 4.0 * (double)g_steps);
+    c.bar_ticks = (uint64_t)(bar_us * res->tick_khz / 1e3);
     const int maxm = maxm_for(m);
     const size_t lds = std::max(knn_xs_bytes(m, d),
                                 sizeof(double) * ((size_t)m * m + m + 16 * k_image_doubles(maxm)));

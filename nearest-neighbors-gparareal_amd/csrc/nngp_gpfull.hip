@@ -36,6 +36,9 @@ namespace nngp {
 #endif
 
 static constexpr int GPB = GPF_PANEL;                // panel width
+// gpf_diag_kernel (two 32x32 blocks per wave, col[32*h+i]), the FULL staging (tid>>5, tid&31) and
+// gpf_update_tile (kq/SU) are written for 32-column panels
+static_assert(GPB == 32, "the full-GP kernels assume 32-column panels");
 static constexpr double GPF_LOG_2PI = 1.8378770664093453;   // np.log(2*np.pi)
 static constexpr int GPF_LDS_ROWS = 7936;            // alpha_kernel keeps the vector in LDS (<= 62 KB) up to here,
                                                      // beyond it in its own output row (no row limit)

@@ -113,7 +113,18 @@ class Parareal(_Parareal):
         self.n = self.u0.shape[0]
 
     def run(self, *args, **kwargs):
-        self.solver.RK_thresh = self.RK_thresh
+        # new_lib's _parareal reads self.Ng / self.Nf / self.F / self.G / self.RK_thresh when it
+        # runs (new_lib.py:902-997), and the scalability scripts re-assign them after construction
+        # (Hopf.py:68-69: s.Nf = s.Nf * 10000; s.RK_thresh = s.Nf/s.N/scaling)
+        s, N = self.solver, self.N
+        Ng, Nf = int(self.Ng), int(self.Nf)
+        if (Ng % N != 0) or (Nf % Ng != 0):
+            raise Exception('Nf must be a multiple of Ng and Ng must be a multiple of N - change time steps!')
+        if self.F not in _lib.TABLEAU or self.G not in _lib.TABLEAU:
+            raise NotImplementedError('Only RK1, RK2, RK4 and RK8 are implemented')
+        s.Ng, s.Nf, s.Ng_total, s.Nf_total = Ng // N, Nf // N, Ng, Nf
+        s.F, s.G = self.F, self.G
+        s.RK_thresh = self.RK_thresh
         return super().run(*args, **kwargs)
 
 

@@ -101,12 +101,22 @@ def shard_bounds(I, N, world, rank):
     return lo, hi, chunk
 
 
-def fine_sweep_sharded(propagate, t, U, UF, I, N, group=None):
+def native_comm_default():
+    """The library's own RCCL communicator (include/nngp.h nngp_comm_*) for the collectives is
+    opt-in -- run(..., native_comm=True) or NNGP_NATIVE_COMM=1 -- until a multi-GPU run has checked
+    it bitwise against torch.distributed's (bench.py --gpus N records that check); by default the
+    collectives are torch.distributed's (RCCL on an NCCL group)."""
+    return os.environ.get('NNGP_NATIVE_COMM') == '1'
+
+
+def fine_sweep_sharded(propagate, t, U, UF, I, N, group=None, native=None):
     """The fine sweep of one Parareal iteration, UF[I+1:N+1] = F(t[I:N], t[I+1:N+1], U[I:N])
     (parareal.py:310-327), sharded over the ranks of `group`: each rank integrates its contiguous
     block with ONE batched launch (`propagate(t0, t1, U0, out)`), then a single all-gather of the
     [chunk][d] end states (RCCL over xGMI; gloo on CPU) gives every rank the full result.  That
-    all-gather is the only collective of the Parareal iteration."""
+    all-gather is the only collective of the Parareal iteration.  native: use the library's
+    communicator (nngp_allgather_states) instead of torch.distributed's (default
+    native_comm_default())."""
     import torch
     dist = torch.distributed
     world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
@@ -129,7 +139,7 @@ def fine_sweep_sharded(propagate, t, U, UF, I, N, group=None):
         send = gathered[rank * chunk:(rank + 1) * chunk]
         if hi > lo:
             propagate(t[lo:hi], t[lo + 1:hi + 1], U[lo:hi].contiguous(), send[:hi - lo])
-        if _lib.comm_for(group):
+        if (native_comm_default() if native is None else native) and _lib.comm_for(group):
             _lib.check(_lib.lib().nngp_allgather_states(send.data_ptr(), gathered.data_ptr(), chunk * n,
                                                         torch.cuda.current_stream().cuda_stream))
         else:
@@ -384,7 +394,7 @@ class Parareal():
     def _fine_sweep(self, torch, t_dev, Uk, UF, I, N, n):
         """uF[I+1:N+1] = F(u[I:N]) -- sharded over ranks when a process group is active."""
         fine_sweep_sharded(lambda a, b, u, out: self.solver.run_F_batch(a, b, u, out=out),
-                           t_dev, Uk, UF, I, N, self.process_group)
+                           t_dev, Uk, UF, I, N, self.process_group, native=self._run_native_comm)
 
     # ------------------------------------------------------------------ correction sweep
     def _correction_sweep(self, torch, model, t_dev, I, N, U1, UG1, UF, UG, X, Y, rows, th0, stream):
@@ -456,7 +466,7 @@ class Parareal():
 
     def _correction_sweep_sharded(self, torch, model, t_dev, I, N, U1, UG1, X, Y, rows, th0, stream):
         """correction_sweep_sharded with the HIP launches.  On an NCCL group with the library's
-        communicator live (and native_comm, default True): ONE native call,
+        communicator live (and native_comm, opt-in: native_comm_default()): ONE native call,
         nngp_correction_sweep_sharded, that issues every slice's G, this rank's coordinates, the
         RCCL all-gather of the predictions and u = preds + uG on the stream with no host round trip.
         Otherwise (gloo: ranks sharing one GPU) the same launches from Python: G via the solver,
@@ -466,9 +476,11 @@ class Parareal():
         m = min(model.n_neighbours(), int(rows))
         jit, jp = _lib.host_doubles(JITTERS)
         nf = model.n_fits
-        if getattr(self, '_run_native_comm', True) and _lib.comm_for(self.process_group) and \
+        if getattr(self, '_run_native_comm', False) and _lib.comm_for(self.process_group) and \
                 not solver.coarse_is_paged():
             world = torch.distributed.get_world_size(self.process_group)
+            if world == 1:   # NNGP_SHARD_EMULATE_RANKS: one process plays W ranks (include/nngp.h)
+                world = max(1, int(os.environ.get('NNGP_SHARD_EMULATE_RANKS', '1')))
             chunk = (n + world - 1) // world
             gather = torch.zeros(world * chunk, dtype=torch.float64, device=U1.device)
             cs = solver.f.csystem(U1.device)
@@ -579,7 +591,7 @@ class Parareal():
         self._run_speculate = int(kwargs.get('speculate', self.speculate))
         self._spec_skip = 0   # auto speculation: iterations left to run without it (_correction_sweep)
         self._run_shard = kwargs.get('shard_corrections', self.shard_corrections)
-        self._run_native_comm = bool(kwargs.get('native_comm', True))
+        self._run_native_comm = bool(kwargs.get('native_comm', native_comm_default()))
         tspan, N, epsilon, n = self.tspan, self.N, self.epsilon, self.n
         solver = self.solver
         verbose = kwargs.get('verbose', self.verbose)

@@ -12,8 +12,9 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
-def run_case(g, case, shard):
-    """The solves compared across world sizes (same call on 1 rank and on N)."""
+def run_case(g, case, shard, native=None):
+    """The solves compared across world sizes (same call on 1 rank and on N).  native: the
+    library's RCCL communicator for the collectives (run(..., native_comm=...))"""
     if case == 'burgers':   # Burgers_perf_across_m.py's slice schedule on a quarter of the span
         ode = g.Burgers(d_x=128, normalization='-11')
         s = g.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
@@ -43,6 +44,8 @@ def run_case(g, case, shard):
         kw = dict(model='parareal')
     if shard is not None:
         kw['shard_corrections'] = shard
+    if native is not None:
+        kw['native_comm'] = native
     r = p.run(**kw)
     return r['k'], np.array(r['conv_int']), r['u']
 

@@ -58,7 +58,10 @@ def test_native_rccl_comm_and_sharded_sweep_one_rank(gpu, tmp_path):
     """The C-ABI's multi-GPU exchange on the box's one GPU: an NCCL (RCCL) process group of one
     rank, the library's communicator created from it (_lib.comm_for), nngp_allgather_states, and
     nngp_correction_sweep_sharded (every slice's G, this rank's coordinates, the RCCL all-gather and
-    u = preds + uG issued natively) -- bitwise the unsharded run, with and without the native path.
+    u = preds + uG issued natively) -- bitwise the unsharded run, with and without the native path,
+    and with the coordinate split of 3, 7 and 8 ranks played in turn by the one process
+    (NNGP_SHARD_EMULATE_RANKS: each rank's block and the partial last one land where the in-place
+    all-gather would put them).
     Several ranks need several GPUs for RCCL (the 8-GPU bench runs them); the orchestration across
     ranks is covered on gloo above."""
     out = str(tmp_path / 'comm.npz')
@@ -85,12 +88,23 @@ x = torch.arange(10, dtype=torch.float64, device="cuda"); y = torch.zeros(10, dt
 _lib.check(L.nngp_allgather_states(x.data_ptr(), y.data_ptr(), 10, torch.cuda.current_stream().cuda_stream))
 torch.cuda.synchronize(); assert torch.equal(x, y)
 k0, c0, u0 = run_case(g, "fhn", None)          # unsharded (world 1)
-k1, c1, u1 = run_case(g, "fhn", True)          # native sharded sweep
+k1, c1, u1 = run_case(g, "fhn", True, native=True)   # native sharded sweep
+same = lambda a, b: bool(np.array_equal(np.nan_to_num(a, nan=7.0), np.nan_to_num(b, nan=7.0)))
+# the coordinate split of W ranks played in turn by this process (NNGP_SHARD_EMULATE_RANKS): every
+# rank's [c0, c1) into its block of the gather buffer, the partial last block included (d = 200:
+# W = 3 -> blocks of 67, 67, 66; W = 7 -> 29 x 6 + 26; W = 8 -> 25 x 8)
+emu = []
+for W in (3, 7, 8):
+    os.environ["NNGP_SHARD_EMULATE_RANKS"] = str(W)
+    kw_, cw_, uw_ = run_case(g, "fhn", True, native=True)
+    emu.append(kw_ == k0 and list(cw_) == list(c0) and same(uw_, u0))
+del os.environ["NNGP_SHARD_EMULATE_RANKS"]
 ode = g.FHN_PDE(d_x=10)
 s = g.SolverRK(ode.get_vector_field(), Ng=5, Nf=100, F="RK8", G="RK4")
 r2 = g.Parareal(ode, s, [0, 8], 16, epsilon=5e-7, verbose=None).run(model="nngp", nn=20, seed=45, early_stop=2,
                                                                   shard_corrections=True, native_comm=False)
 np.savez(sys.argv[1], k=[k0, k1, r2["k"]], same_native=np.array_equal(np.nan_to_num(u0, nan=7.0), np.nan_to_num(u1, nan=7.0)),
+         emulated=np.array(emu),
          same_py=np.array_equal(np.nan_to_num(u0, nan=7.0), np.nan_to_num(r2["u"], nan=7.0)),
          conv=[list(c0) == list(c1), list(c0) == list(r2["conv_int"])])
 torch.distributed.destroy_process_group()
@@ -102,3 +116,4 @@ print("comm ok")
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
     R = np.load(out)
     assert len(set(R['k'].tolist())) == 1 and bool(R['same_native']) and bool(R['same_py']) and all(R['conv'])
+    assert R['emulated'].tolist() == [True, True, True], R['emulated']

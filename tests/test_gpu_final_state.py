@@ -51,6 +51,9 @@ def test_burgers_n128_seeds_bitwise_oracle_loop_and_final_state(gpu):
         err = float(np.max(np.abs(r['u'][:, :, -1] - fine)))
         print(f'seed {seed}: K={r["k"]} (oracle {int(P["k"][j])}) final-state error {err:.3e}')
         assert r['converged'] and r['k'] == int(P['k'][j]) and r['conv_int'] == conv
+        # against the reference itself: its 100 recorded seeds on this schedule all gave K in
+        # {9, 10} (Burges_nngp_exp_val_speed, T = 5, m = 15: 68 x 9, 32 x 10)
+        assert r['k'] in (9, 10)
         assert _digest(r['u']) == str(P['digest'][j])
         assert err <= 1e-6   # BASELINE configs[2]: fp64 tol 1e-6
 
@@ -59,9 +62,11 @@ def test_burgers_n128_seeds_bitwise_oracle_loop_and_final_state(gpu):
 @pytest.mark.timeout(600)
 def test_burgers_n128_k_distribution_100_seeds(gpu):
     """configs[2] over 100 seeds (0-99): every run converges, within 1e-6 of the serial fine
-    solution, in K in {8..11}; the share of K = 9 is within 0.2 of the reference's 68/100 (a
-    two-sample bound: the standard error of the difference of two 100-run shares at p = 0.68 is
-    0.066, so 0.2 is three of them)."""
+    solution, in K in {9, 10} as all of the reference's 100 seeds did -- except at most two runs
+    at K = 11 (round 4 recorded one of 100: profiles/r04/parity_r4a.txt; a threshold straddle of
+    the last unconverged slice, which this test prints) -- and the share of K = 9 is within 0.2 of
+    the reference's 68/100 (a two-sample bound: the standard error of the difference of two
+    100-run shares at p = 0.68 is 0.066, so 0.2 is three of them)."""
     fine = golden('burgers128_seeds.npz')['fine']
     ks, errs = [], []
     for seed in range(100):
@@ -69,10 +74,14 @@ def test_burgers_n128_k_distribution_100_seeds(gpu):
         assert r['converged']
         ks.append(r['k'])
         errs.append(float(np.max(np.abs(r['u'][:, :, -1] - fine))))
+        if r['k'] not in (9, 10):
+            em = [float(np.nanmax(r['err'][:, k])) for k in range(r['k'])]
+            print(f'seed {seed}: K={r["k"]} conv_int {r["conv_int"]} per-iteration max err '
+                  f'{[f"{v:.3g}" for v in em]} (epsilon 5e-7)')
     hist = {k: ks.count(k) for k in sorted(set(ks))}
     print('K histogram over seeds 0-99:', hist, '(reference, its 100 seeds: {9: 68, 10: 32}); '
           f'final-state error max {max(errs):.3e}, median {np.median(errs):.3e}')
-    assert set(ks) <= {8, 9, 10, 11}
+    assert set(ks) <= {9, 10, 11} and ks.count(11) <= 2
     assert abs(ks.count(9) / 100 - 0.68) <= 0.2
     assert max(errs) <= 1e-6
 

@@ -40,8 +40,12 @@ KNOBS = [
     ('fhn512', 'NNGP_RK_THREADS', '512'), ('lorenz', 'NNGP_RK_GROUP', '0'), ('lorenz', 'NNGP_CHAIN', '1'),
     ('lorenz', 'NNGP_NM_LEVEL2', '0'), ('fhn512', 'NNGP_RESUME_W4', '0'), ('fhn512', 'NNGP_RESUME_W4', '100000'),
     ('fhn512', 'NNGP_RESUME_W2', '0'), ('burgers', 'NNGP_SPEC_WAIT_US', '0'), ('burgers', 'NNGP_GUESS_FUSED', '0'),
-    ('lorenz', 'NNGP_GUESS_FUSED', '0'),
+    ('lorenz', 'NNGP_GUESS_FUSED', '0'), ('lorenz', 'NNGP_CHAIN_BARRIER_US', '0'),
 ]
+# knobs whose neutrality needs a setting these runs do not have, tested where they apply:
+# NNGP_SHARD_EMULATE_RANKS (a one-rank RCCL communicator: test_gpu_distributed.py
+# ::test_native_rccl_comm_and_sharded_sweep_one_rank plays 3, 7 and 8 ranks against the unsharded run)
+COVERED_ELSEWHERE = ['NNGP_SHARD_EMULATE_RANKS']
 
 
 @pytest.mark.parametrize('case,knob,value', KNOBS)
@@ -52,6 +56,10 @@ def test_knob_is_bitwise_neutral(gpu, case, knob, value, monkeypatch):
     monkeypatch.setenv(knob, value)
     if knob == 'NNGP_CHAIN':
         monkeypatch.setenv('NNGP_CHAIN_PROF', '1')   # the chain's per-phase clocks must not change a bit either
+    if knob == 'NNGP_CHAIN_BARRIER_US':
+        # the chain's grid-barrier timeout at its floor (4 us per G step: 24 us for Lorenz) -- a
+        # barrier that times out reruns the sweep on the launch chain, the same bits
+        monkeypatch.setenv('NNGP_CHAIN', '1')
     k1, c1, u1 = _run(gpu, case)
     assert (k1, c1) == (k0, c0)
     assert np.array_equal(u1, u0)

@@ -1,0 +1,41 @@
+"""Run entries of the reference's published K table (tests/published_k.py) on the GPU and record
+K, conv_int, the per-iteration error maxima and timings, one JSON file per entry under
+gpurun_out/published_k/ (copied to profiles/r05/ afterwards).
+
+    python -u tools/published_k_run.py fhn10_512_para fhn10_512_nngp hopf_512_nngp ...
+
+Progress goes to stdout every iteration (verbose driver), so a long entry is never silent."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, 'tests')]
+
+import published_k as P   # noqa: E402
+
+
+def main(names):
+    import torch
+    import nngp_amd as gpu
+    torch.cuda.set_device(0)
+    out_dir = os.path.join(ROOT, 'gpurun_out', 'published_k')
+    os.makedirs(out_dir, exist_ok=True)
+    for name in names:
+        s, kw, pk = P.build(gpu, name, verbose='v')
+        print(f'=== {name}: published K {pk}; run kwargs {kw}; Nf/N {s.Nf // s.N}, RK_thresh {s.RK_thresh}',
+              flush=True)
+        t0 = time.time()
+        r = s.run(**kw)
+        summ = P.summarise(r)
+        summ.update(name=name, published_K=pk, wall_s=time.time() - t0, Nf_per_slice=s.Nf // s.N,
+                    Ng_per_slice=s.Ng // s.N, RK_thresh=s.RK_thresh, run_kwargs={k: v for k, v in kw.items()},
+                    spec_hits=r['timings'].get('spec_hits'))
+        with open(os.path.join(out_dir, name + '.json'), 'w') as f:
+            json.dump(summ, f, indent=1)
+        print('RESULT', json.dumps(summ), flush=True)
+
+
+if __name__ == '__main__':
+    main(sys.argv[1:])
