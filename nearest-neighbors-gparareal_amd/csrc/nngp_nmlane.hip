@@ -1,0 +1,399 @@
+// nngp_nmlane.hip -- the throughput-shaped Nelder-Mead fits kernel: LPF (2 or 4) lanes per fit,
+// the exact neighbour count M as a compile-time constant (no padding).
+//
+// Reference: NNGP_p.get_preds fans d*9*R independent fits out through pool.map (models.py:185-202);
+// each is scipy's Nelder-Mead (models.py:254-260) on the -LML of _fit_gp_jit (models.py:86-92,
+// 240-252).  The speculative correction sweep (nngp_sweep.hip) batches every slice's fits of one
+// Parareal iteration into ONE launch -- Burgers N = 128: 128 predictions x 1 152 fits = 147 456
+// independent fits.  That is throughput work; nm_fit_kernel (nngp_gp.hip) runs a fit on a 16-lane
+// DPP row, a layout built for the latency of one fit (~1 830 VALU per wave-evaluation of 4 fits,
+// ~29 k issued lane-slots per fit-evaluation, profiles/r04/pmc_burgers_nm_r4c.txt).  Here a fit
+// owns LPF lanes of a wave (a quad, or a pair inside one):
+//   * lane q holds rows q, q+LPF, q+2 LPF, ... of the M x M kernel matrix (slot s = row / LPF) in
+//     VGPRs, only the lower-triangle columns a slot can have (k < LPF s + LPF);
+//   * the triangle's exps are the owners' own (no redistribution);
+//   * the left-looking Cholesky broadcasts row j's entries L_jk from its owner lane by one
+//     quad_perm DPP move (two v_mov_b32_dpp per double) and every lane updates its own rows;
+//   * the forward solve runs fused into the columns; the back solve reads the transposed L from a
+//     per-fit LDS image (each lane writes its rows once);
+//   * the -LML sums use the oracle's butterfly order: xor-partner DPP levels inside the group,
+//     the remaining levels inside the lane.
+// Every row's arithmetic is the oracle's gp_factor / orc_nlml (oracle/nngp_oracle.c) in the same
+// order -- OpenBLAS dpotf2_L's ddot pivot and dgemv_n vector/tail rows, successive-subtraction
+// solves with Markstein quotients, the 16-slot butterfly sums -- so the fits are bitwise the
+// packed kernel's and the oracle's (tests/test_gpu_kernels.py::test_nm_lanes_kernel_*).
+#include <math.h>
+
+#include <algorithm>
+
+#include "common.h"
+#include "nngp_gpeval.h"
+#include "nngp_math.h"
+#include "nngp_nm.h"
+#include "nngp_nmargs.h"
+
+namespace nngp {
+
+template <int M, int LPF> struct LaneFit {
+    static_assert(LPF == 2 || LPF == 4, "2 or 4 lanes per fit");
+    static constexpr int RPL = (M + LPF - 1) / LPF;          // row slots per lane
+    static constexpr int NB = 16 / LPF;                      // slots of the 16-entry butterfly
+    // columns slot s can hold: rows LPF s .. LPF s + LPF - 1 have entries k <= row
+    static constexpr int ncol(int s) { return LPF * s + LPF < M ? LPF * s + LPF : M; }
+    // the back solve's LDS image of L, per fit: entry (slot s, column k) of lane q at
+    // (off(s, k)) LPF + q -- every lane's addresses are its base plus compile-time offsets
+    static constexpr int off(int s, int k) { return s == 0 ? k : off(s - 1, ncol(s - 1)) + k; }
+    static constexpr int IMG = (off(RPL - 1, ncol(RPL - 1)) + LPF) * LPF;   // (+ a slot of padding)
+    // dpotf2's tail rows of column j start here (the last (M-1-j) & 3 rows under j)
+    static constexpr int tail_start(int j) { return j + 1 + ((M - 1 - j) & ~3); }
+};
+
+// every lane of the group <- lane SRC of the group (quad_perm)
+template <int LPF, int SRC, typename T>
+__device__ __forceinline__ T gbcast(T v) {
+    if constexpr (LPF == 4) {
+        return __builtin_amdgcn_mov_dpp(v, SRC | (SRC << 2) | (SRC << 4) | (SRC << 6), 0xF, 0xF, false);
+    } else {
+        return __builtin_amdgcn_mov_dpp(v, SRC | (SRC << 2) | ((2 + SRC) << 4) | ((2 + SRC) << 6), 0xF, 0xF, false);
+    }
+}
+
+// xor partner inside the group: 1 -> quad_perm [1,0,3,2], 2 -> [2,3,0,1]
+template <int X>
+__device__ __forceinline__ double xor_dpp(double v) {
+    return __builtin_amdgcn_mov_dpp(v, X == 1 ? 0xB1 : 0x4E, 0xF, 0xF, false);
+}
+
+// x / L_ii as the oracle's Markstein quotient: q = x RN(1/L_ii), fma(fma(-q, L_ii, x), RN(1/L_ii), q)
+__device__ __forceinline__ double mk_div(double x, double lii, double ri) {
+    const double q = x * ri;
+    return fma(fma(-q, lii, x), ri, q);
+}
+
+// ljj = sqrt(x), ri = 1.0/ljj, both correctly rounded, for every x > 0 (the pivots that pass):
+// the short mid-range sequences (nngp_math.h sqrt_mid / rcp_mid, exact on [2^-500, 2^500]) on x
+// scaled by 4^k, k in {300, 0, -300}, and the results scaled back by 2^-k / 2^k -- exact, since
+// sqrt(x 4^k) = sqrt(x) 2^k and both results stay normal (sqrt(x) in [2^-537, 2^512]).  x = +inf
+// gives (inf, 0) as sqrt / division do.  Branch-free: a uniform branch to the full sequences was
+// if-converted by LLVM, which then ran both (and held both's registers) at every column.
+__device__ __forceinline__ void sqrt_rcp_exact(double x, double &ljj, double &ri) {
+    const int k = x < 0x1p-500 ? 300 : (x > 0x1p+500 ? -300 : 0);
+    const double s = sqrt_mid(ldexp(x, 2 * k));
+    const double r = rcp_mid(s);
+    const bool inf = x == __builtin_huge_val();
+    ljj = inf ? x : ldexp(s, -k);
+    ri = inf ? 0.0 : ldexp(r, k);
+}
+
+// oracle butterfly_sum over the fit's rows r < M of v[r] (row r = LPF s + q in slot s of lane q):
+// fold rows >= 16 into rows r mod 16 (adding the oracle's 0.0 for missing ones), then levels
+// 1, 2, 4, 8 -- the ones below LPF across the group's lanes, the rest inside the lane
+template <int M, int LPF>
+__device__ __forceinline__ double lane_bsum(const double (&v)[LaneFit<M, LPF>::RPL], int q) {
+    constexpr int NB = LaneFit<M, LPF>::NB, RPL = LaneFit<M, LPF>::RPL;
+    double p[NB];
+#pragma unroll
+    for (int s = 0; s < NB; s++) {
+        p[s] = (s < RPL && LPF * s + q < M) ? v[s < RPL ? s : 0] : 0.0;
+#pragma unroll
+        for (int f = 1; 16 * f < M; f++) {
+            const int s2 = s + f * NB;
+            p[s] = p[s] + ((s2 < RPL && LPF * s2 + q < M) ? v[s2 < RPL ? s2 : 0] : 0.0);
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < NB; s++) {
+        p[s] = p[s] + xor_dpp<1>(p[s]);
+        if constexpr (LPF == 4) p[s] = p[s] + xor_dpp<2>(p[s]);
+    }
+#pragma unroll
+    for (int st = 1; st < NB; st <<= 1)
+#pragma unroll
+        for (int s = 0; s < NB; s += 2 * st) p[s] = p[s] + p[s + st];
+    return p[0];
+}
+
+// -LML (models.py:240-252) of the fit this lane's group owns at (sx, sy); +inf on NaN or a failed
+// Cholesky.  ys: the group's y rows of this lane; sD2: [M][M]; img: the group's LDS image.
+template <int M, int LPF>
+__device__ __forceinline__ double lane_nlml(int q, const double *sD2, double sx, double sy, double jit,
+                                            const double (&ys)[LaneFit<M, LPF>::RPL], double *img) {
+    using LF = LaneFit<M, LPF>;
+    constexpr int RPL = LF::RPL;
+    const double c = -0.5 * (1 / nn_pow10(sx));
+    const double psy = nn_pow10(sy);
+    double a[RPL][M];
+    // the owners' triangle entries: K_rk = psy exp(c D2_rk) (+ jit on the diagonal), models.py:146-155, 88
+    // (D2 row LPF s + q at this lane's base q M plus a constant; rows >= M read harmless LDS)
+    // The exps run as a chain, at most two in flight: entry t's D2 load waits (a "memory" pin)
+    // until entry t-2's exp is done.  Left free, LLVM interleaves all ~40 independent exps of the
+    // lane for ILP and holds their ~6 VGPRs each at once (256 VGPRs + 194 AGPRs at M = 15); a wave's
+    // dependent fp64 ops issue as fast as independent ones (tools/ubench_fp64.hip), so nothing is lost.
+    const double *d2q = sD2 + q * M;
+    double e1 = 0.0, e2 = 0.0;   // the last two entries
+#pragma unroll
+    for (int s = 0; s < RPL; s++) {
+#pragma unroll
+        for (int k = 0; k < M; k++) {
+            if (k >= LF::ncol(s)) continue;
+            asm volatile("" ::"v"(e2) : "memory");
+            double e = psy * nn_exp_nonpos(c * d2q[LPF * s * M + k]);
+            if (k >= LPF * s) e = (k == LPF * s + q) ? e + jit : e;
+            a[s][k] = e;
+            e2 = e1;
+            e1 = e;
+        }
+    }
+    double acc[RPL], dg[RPL], rv[RPL];
+#pragma unroll
+    for (int s = 0; s < RPL; s++) {
+        acc[s] = ys[s];
+        dg[s] = 1.0;
+        rv[s] = 1.0;
+    }
+    bool bad = false;
+    static_for<0, M>([&](auto jc) {
+        constexpr int j = decltype(jc)::value, SJ = j / LPF, QJ = j % LPF;
+        constexpr int TS = LF::tail_start(j), JB = j & ~3;
+        // pivot: a_jj - ddot(row j) (potf2_dot: two accumulators over groups of 4, fma tail)
+        double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+        for (int k = 0; k + 4 <= j; k += 4) {
+            t1 = t1 + fma(a[SJ][k], a[SJ][k], a[SJ][k + 2] * a[SJ][k + 2]);
+            t2 = t2 + fma(a[SJ][k + 1], a[SJ][k + 1], a[SJ][k + 3] * a[SJ][k + 3]);
+        }
+#pragma unroll
+        for (int k = JB; k < j; k++) t1 = fma(a[SJ][k], a[SJ][k], t1);
+        const double pv = gbcast<LPF, QJ>(a[SJ][j] - (t1 + t2));
+        bad = bad || !(pv > 0.0);
+        double ljj, ri;
+        sqrt_rcp_exact(pv, ljj, ri);
+        dg[SJ] = (q == QJ) ? ljj : dg[SJ];
+        rv[SJ] = (q == QJ) ? ri : rv[SJ];
+        // rows below j (dgemv_n, then * RN(1/ajj)): vector rows y -= 4-column fma blocks, leftover
+        // columns y -= a x; tail rows y -= one fma chain.  x_k = L_jk from the owner, k ascending.
+        double yv[RPL], bk[RPL], tt[RPL];
+#pragma unroll
+        for (int s = SJ; s < RPL; s++) {
+            yv[s] = a[s][j];
+            bk[s] = 0.0;
+            tt[s] = 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < j; k++) {
+            const double xk = gbcast<LPF, QJ>(a[SJ][k]);
+#pragma unroll
+            for (int s = SJ; s < RPL; s++) {
+                const bool vec = LPF * s < TS, tail = LPF * s + LPF - 1 >= TS;
+                const double ak = a[s][k];
+                if (vec) {
+                    if (k < JB) {
+                        bk[s] = (k % 4 == 0) ? ak * xk : fma(ak, xk, bk[s]);
+                        if (k % 4 == 3) yv[s] = yv[s] - bk[s];
+                    } else {
+                        yv[s] = yv[s] - ak * xk;
+                    }
+                }
+                if (tail) tt[s] = fma(ak, xk, tt[s]);
+            }
+        }
+#pragma unroll
+        for (int s = SJ; s < RPL; s++) {
+            const bool vec = LPF * s < TS, tail = LPF * s + LPF - 1 >= TS;
+            double y = vec ? yv[s] : a[s][j] - tt[s];
+            if (vec && tail) y = (LPF * s + q < TS) ? yv[s] : a[s][j] - tt[s];
+            // rows <= j of slot SJ keep what they hold (the owner's diagonal K_jj is no longer read)
+            a[s][j] = (s > SJ || q > QJ) ? y * ri : a[s][j];
+        }
+        // forward solve, fused: z_j = acc_j / L_jj, then rows below subtract L_ij z_j (models.py:90)
+        const double zj = mk_div(gbcast<LPF, QJ>(acc[SJ]), ljj, ri);
+        acc[SJ] = (q == QJ) ? zj : acc[SJ];   // acc of row j becomes z_j
+#pragma unroll
+        for (int s = SJ; s < RPL; s++) {
+            if (s > SJ) acc[s] = acc[s] - a[s][j] * zj;
+            else acc[s] = (q > QJ) ? acc[s] - a[s][j] * zj : acc[s];
+        }
+    });
+    // back solve L^T alpha = z: the lanes' rows of L into the fit's LDS image, then alpha_i
+    // (descending) from its owner, and every lane subtracts L_ir alpha_i from its rows r < i (k
+    // descending, the oracle's order), L_ir read back from the image.  The image is rewritten every
+    // evaluation: the first sync orders these writes after the previous evaluation's reads.
+    wave_lds_sync();
+    double *imw = img + q;
+#pragma unroll
+    for (int s = 0; s < RPL; s++)
+#pragma unroll
+        for (int k = 0; k < M - 1; k++)
+            if (k < LF::ncol(s)) imw[LF::off(s, k) * LPF] = a[s][k];
+    wave_lds_sync();
+    const double *imr = img + q * LPF;   // + (off(SI, LPF s) ) LPF + QI: row i's column LPF s + q
+    double al[RPL];
+#pragma unroll
+    for (int s = 0; s < RPL; s++) al[s] = 0.0;
+    static_for<0, M>([&](auto ic) {
+        constexpr int i = M - 1 - decltype(ic)::value, SI = i / LPF, QI = i % LPF;
+        const double ai = gbcast<LPF, QI>(mk_div(acc[SI], dg[SI], rv[SI]));
+        al[SI] = (q == QI) ? ai : al[SI];
+#pragma unroll
+        for (int s = 0; s <= SI; s++) {
+            if (LPF * s >= i) continue;   // no row of the slot is below i
+            const double lir = imr[LF::off(SI, LPF * s) * LPF + QI];
+            if (LPF * s + LPF - 1 < i) acc[s] = acc[s] - lir * ai;
+            else acc[s] = (LPF * s + q < i) ? acc[s] - lir * ai : acc[s];
+        }
+    });
+    double ya[RPL], lg[RPL];
+#pragma unroll
+    for (int s = 0; s < RPL; s++) {
+        ya[s] = ys[s] * al[s];
+        lg[s] = nn_log(dg[s]);
+    }
+    const double ydot = lane_bsum<M, LPF>(ya, q);
+    const double slog = lane_bsum<M, LPF>(lg, q);
+    const double res = -(((-0.5 * ydot) - slog) - ((double)M / 2) * LOG_2PI);
+    // every lane of the group has the same bits: the pivots and sums are broadcast / symmetric
+    return (bad || res != res) ? INFINITY : res;
+}
+
+// One fit per LPF lanes; unfused batched mode (blockIdx.y = prediction, product-order fits or
+// explicit coord / jitter arrays), work queue per prediction.
+template <int M, int LPF>
+__global__ void __launch_bounds__(256) nm_lane_kernel(NMArgs a) {
+    using LF = LaneFit<M, LPF>;
+    constexpr int RPL = LF::RPL;
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    if (a.skip && *a.skip) return;
+    nm_batch_offsets(a);
+    const int nfc = a.nj * a.R;
+    const int ngroups = blockDim.x / LPF;
+    double *sD2 = sm;
+    double *sImg = sD2 + M * M;
+    __shared__ double sJit[MAX_JIT];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < M * M; i += blockDim.x) sD2[i] = a.D2[i];
+    if (tid < MAX_JIT) sJit[tid] = jit_lookup(a, tid);
+    __syncthreads();
+    const int g = tid / LPF;
+    int q = tid % LPF;
+    asm volatile("" : "+v"(q));   // opaque: per-column lane masks stay one compare where used
+    double *img = sImg + (size_t)g * LF::IMG;
+    NMCfg cfg{a.fatol, a.xatol, a.maxfev, a.maxfev};
+    NM St;
+    double ys[RPL];
+    double jit = 1.0;
+    int fn = blockIdx.x * ngroups + g, f = 0;
+    bool valid = false;
+    auto start_fit = [&]() {
+        valid = fn < a.n_fits;
+        f = fn;
+        if (valid && a.jmajor && !a.coord) f = (fn % a.d) * nfc + fn / a.d;
+        int coord = 0, jidx = 0;
+        if (valid) {
+            if (a.coord) {
+                coord = a.coord[f];
+                jidx = a.jitter_idx[f];
+            } else {   // product(coord, jitter, restart) order (models.py:186)
+                coord = f / nfc;
+                jidx = (f % nfc) / a.R;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < RPL; s++) {
+            const int row = LPF * s + q;
+            ys[s] = (valid && row < M) ? a.Y[(int64_t)coord * a.ys_c + (int64_t)row * a.ys_r] : 0.0;
+        }
+        jit = valid ? sJit[jidx] : 1.0;
+        St.f0 = St.f1 = St.f2 = INFINITY;
+        St.xbx = St.xby = St.xrx = St.xry = St.fxr = 0.0;
+        if (valid) {
+            nm_start(St, cfg, a.theta0[2 * f], a.theta0[2 * f + 1]);
+        } else {
+            St.s0x = St.s0y = St.s1x = St.s1y = St.s2x = St.s2y = 0.0;
+            St.px = St.py = 0.0;
+            St.fcalls = St.iters = 0;
+            St.st = ST_DONE;
+        }
+    };
+    auto write_fit = [&]() {
+        if (!valid || q != 0) return;
+        const double fval = (St.f1 != St.f1 || St.f2 != St.f2) ? NAN : St.f0;
+        if (a.theta_out) { a.theta_out[2 * f] = St.s0x; a.theta_out[2 * f + 1] = St.s0y; }
+        if (a.fval_out) a.fval_out[f] = fval;
+        if (a.nfev_out) a.nfev_out[f] = St.fcalls;
+        if (a.fits_out) {
+            a.fits_out[4 * f + 0] = St.s0x;
+            a.fits_out[4 * f + 1] = St.s0y;
+            a.fits_out[4 * f + 2] = fval;
+            a.fits_out[4 * f + 3] = (double)St.fcalls;
+        }
+        if (a.done) {   // the fit is visible device-wide before it is counted
+            __threadfence();
+            __hip_atomic_fetch_add(a.done + blockIdx.y, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+    start_fit();
+    bool can_take = a.queue != nullptr && valid;
+    // every group of the wave evaluates once per trip until the wave's last fit is done (finished
+    // groups evaluate a dummy point, so the evaluation never diverges); a finished group first
+    // takes the next unassigned fit of its prediction from the queue
+    while (true) {
+        if (can_take && St.st == ST_DONE) {   // uniform within the group
+            write_fit();
+            int nf = 0;
+            if (q == 0) nf = (int)(gridDim.x * ngroups) + atomicAdd(a.queue + blockIdx.y, 1);
+            fn = gbcast<LPF, 0>(nf);
+            start_fit();
+            can_take = valid;
+        }
+        const bool need = St.st != ST_DONE;
+        if (!__any(need)) break;
+        const double fv = lane_nlml<M, LPF>(q, sD2, St.px, St.py, jit, ys, img);
+        if (need) nm_consume(St, cfg, fv);
+    }
+    write_fit();
+}
+
+// instantiated neighbour counts: the speculative batches of the BASELINE configs (Burgers nn = 15,
+// Hopf / Lorenz 10-15), four lanes per fit.  (m >= 17 would need more than a lane's 256 VGPRs at
+// LPF = 4 -- the packed kernel serves it.)
+template <int M> struct LaneLPF { static constexpr int V = 4; };
+
+template <typename F>
+static int with_lane_m(int m, F &&f) {
+    switch (m) {
+    case 10: return f(std::integral_constant<int, 10>{});
+    case 15: return f(std::integral_constant<int, 15>{});
+    default: return NNGP_E_UNSUPPORTED;
+    }
+}
+
+bool nm_lanes_supported(int m) {
+    return with_lane_m(m, [](auto) { return NNGP_OK; }) == NNGP_OK;
+}
+
+int run_nm_lanes(NMArgs &a, hipStream_t st, int nq, int qslot) {
+    return with_lane_m(a.m, [&](auto mc) {
+        constexpr int M = decltype(mc)::value, LPF = LaneLPF<M>::V;
+        // workgroup size (NNGP_NM_LANES_WG: 64 / 128 / 256): the kernel runs one wave per SIMD
+        // (its VGPRs), so smaller workgroups free a SIMD as soon as their wave's fits are done
+        const int wg = env_int("NNGP_NM_LANES_WG", 256);
+        const int threads = (wg == 64 || wg == 128) ? wg : 256, ngroups = threads / LPF;
+        const size_t lds = sizeof(double) * ((size_t)M * M + (size_t)ngroups * LaneFit<M, LPF>::IMG);
+        int nblocks = (a.n_fits + ngroups - 1) / ngroups;
+        a.queue = nullptr;
+        const int per_group = std::max(0, env_int("NNGP_NM_REFILL", 8));
+        if (per_group > 1 && nblocks > 1) {   // work queues: ~per_group fits per group on average
+            int err = 0;
+            int32_t *qbuf = (int32_t *)workspace(sizeof(int32_t) * (size_t)nq, &err, qslot);
+            if (err) return err;
+            NNGP_HIP_CHECK(hipMemsetAsync(qbuf, 0, sizeof(int32_t) * (size_t)nq, st));
+            a.queue = qbuf;
+            nblocks = std::max(1, (nblocks + per_group - 1) / per_group);
+        }
+        hipLaunchKernelGGL((nm_lane_kernel<M, LPF>), dim3(nblocks, nq), dim3(threads), lds, st, a);
+        NNGP_LAUNCH_CHECK();
+        return NNGP_OK;
+    });
+}
+
+}  // namespace nngp

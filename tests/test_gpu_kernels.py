@@ -260,6 +260,32 @@ def test_nm_fit_batch_vs_oracle(gpu, m, d, tol):
     assert exact == len(coords)   # shared exp/log/10^x: bitwise
 
 
+@pytest.mark.parametrize('m,d,dup', [(10, 3, False), (15, 3, True), (15, 128, False), (15, 128, True)])
+def test_nm_lanes_kernel_vs_oracle(gpu, m, d, dup, monkeypatch):
+    """The throughput fits kernel (csrc/nngp_nmlane.hip: 4 lanes per fit, exact m, work queue;
+    forced by NNGP_NM_LANES=1) through nngp_nm_fit_batch: every fit -- theta, -LML and nfev -- bit
+    for bit the oracle's Nelder-Mead (oracle/nngp_oracle.c orc_nm_fit).  d = 128: all 1 152
+    (coordinate, jitter) fits of a Burgers-sized prediction; dup: two neighbours coincide, so the
+    low-jitter kernels are singular and their Cholesky fails (NaN -> +inf) on the way."""
+    monkeypatch.setenv('NNGP_NM_LANES', '1')
+    mdl = gpu.NNGP_p(n=d, N=4, fatol=0.1, xatol=0.1, seed=7)
+    xm, ym = _nm_case(m, d, m * 100 + d + 1)
+    if dup:
+        xm[m - 1] = xm[1]
+    coords = [c for c in range(d) for _ in range(9)]
+    jidx = [j for _ in range(d) for j in range(9)]
+    th0 = mdl.draw_thetas(1)[:len(coords)]
+    res = mdl.fit_batch(xm, ym, coords, jidx, th0)
+    D2 = O.d2_matrix(xm)
+    bad = []
+    for f in range(len(coords)):
+        th, fv, ne = O.nm_fit(D2, ym[:, coords[f]], th0[f], gpu.models.JITTERS[jidx[f]], 0.1, 0.1)
+        if not (ne == res['nfev'][f] and np.array_equal(th, res['theta'][f]) and
+                (fv == res['fval'][f] or (np.isnan(fv) and np.isnan(res['fval'][f])))):
+            bad.append((f, ne, res['nfev'][f], fv, res['fval'][f]))
+    assert not bad, bad[:5]
+
+
 def test_gp_mean_vs_oracle(gpu):
     L = golden('lml.npz')
     mdl = gpu.NNGP_p(n=3, N=4)
