@@ -554,6 +554,17 @@ static double nn_exp_dd(double hi, double lo) {
 
 double nn_exp(double x) { return nn_exp_dd(x, 0.0); }
 
+/* elementwise nn_exp / nn_log over arrays (tools/fit_agreement.py)                          */
+void orc_exp_array(int64_t n, const double *x, double *out) {
+    for (int64_t i = 0; i < n; i++) out[i] = nn_exp(x[i]);
+}
+
+double nn_log(double x);
+
+void orc_log_array(int64_t n, const double *x, double *out) {
+    for (int64_t i = 0; i < n; i++) out[i] = nn_log(x[i]);
+}
+
 double nn_pow10(double x) {
     const double hi = x * NN_LN10;
     const double lo = fma(x, NN_LN10, -hi) + x * NN_LN10_LO;
@@ -776,16 +787,9 @@ void orc_set_sum_order(int o) { g_sum_order = o; }
  * passes on exactly duplicated neighbours -- FHN-PDE at its steady state -- derailed the run).
  * The solves: forward z_i (k ascending), back alpha_i (k descending), successive subtraction,
  * each division the Markstein-corrected x*RN(1/L_ii) (bitwise the IEEE quotient).            */
-static int gp_factor(int m, const double *D2, const double *y, double c, double psy, double jit,
-                     double *L /*m*m*/, double *alpha) {
-    /* build lower triangle (models.py:146-155, 88) */
-    for (int r = 0; r < m; r++)
-        for (int j = 0; j <= r; j++) {
-            double v = psy * nn_exp(c * D2[r * m + j]);
-            if (j == r) v = v + jit;
-            L[r * m + j] = v;
-        }
-    double rinv_d[64];
+/* the factorisation and the two solves on a built K (lower triangle of L, in place), exported as
+ * orc_potf2 / orc_solves for the fit-level attribution (tools/fit_agreement.py)                */
+int orc_potf2(int m, double *L /*m*m, lower = K on entry*/, double *rinv_d) {
     for (int j = 0; j < m; j++) {
         const double t = L[j * m + j] - potf2_dot(L + j * m, j);
         if (!(t > 0.0)) return 1;           /* ajj <= 0 or NaN: jax -> NaN -> +inf          */
@@ -797,6 +801,31 @@ static int gp_factor(int m, const double *D2, const double *y, double c, double 
         for (int i = j + 1; i < m; i++)
             L[i * m + j] = potf2_gemv_row(L[i * m + j], L + i * m, L + j * m, j, i - j - 1 < m1) * rinv;
     }
+    return 0;
+}
+
+static void gp_solves(int m, const double *L, const double *rinv_d, const double *y, double *alpha);
+
+void orc_solves(int m, const double *L, const double *rinv_d, const double *y, double *alpha) {
+    gp_solves(m, L, rinv_d, y, alpha);
+}
+
+static int gp_factor(int m, const double *D2, const double *y, double c, double psy, double jit,
+                     double *L /*m*m*/, double *alpha) {
+    /* build lower triangle (models.py:146-155, 88) */
+    for (int r = 0; r < m; r++)
+        for (int j = 0; j <= r; j++) {
+            double v = psy * nn_exp(c * D2[r * m + j]);
+            if (j == r) v = v + jit;
+            L[r * m + j] = v;
+        }
+    double rinv_d[64];
+    if (orc_potf2(m, L, rinv_d)) return 1;
+    gp_solves(m, L, rinv_d, y, alpha);
+    return 0;
+}
+
+static void gp_solves(int m, const double *L, const double *rinv_d, const double *y, double *alpha) {
     double z[64];
     for (int i = 0; i < m; i++) {
         double s = y[i];
@@ -820,7 +849,6 @@ static int gp_factor(int m, const double *D2, const double *y, double c, double 
         const double q = s * rinv_d[i];
         alpha[i] = fma(fma(-q, L[i * m + i], s), rinv_d[i], q);
     }
-    return 0;
 }
 
 static const double LOG_2PI = 1.8378770664093453; /* np.log(2*np.pi) */

@@ -77,6 +77,11 @@ def lib():
         L.orc_d2.argtypes = [_dp, i32, i32, _dp]
         L.orc_max_threads.restype = ctypes.c_int
         L.orc_set_sum_order.argtypes = [i32]
+        L.orc_potf2.argtypes = [i32, _dp, _dp]
+        L.orc_potf2.restype = i32
+        L.orc_solves.argtypes = [i32, _dp, _dp, _dp, _dp]
+        L.orc_exp_array.argtypes = [i64, _dp, _dp]
+        L.orc_log_array.argtypes = [i64, _dp, _dp]
         for fn in ('nn_exp', 'nn_log', 'nn_pow10', 'nn_sin', 'nn_cos', 'nn_sin_pi'):
             getattr(L, fn).argtypes = [dbl]
             getattr(L, fn).restype = dbl

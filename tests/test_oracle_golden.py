@@ -122,8 +122,13 @@ def test_nlml_matches_reference():
     assert np.array_equal(np.isinf(v), np.isinf(ref))
     both = np.isfinite(v) & np.isfinite(ref)
     rel = np.abs(v[both] - ref[both]) / np.maximum(1, np.abs(ref[both]))
-    assert rel.max() < 1e-6
-    assert np.median(rel) < 1e-14
+    print(f'-LML vs the reference over {both.sum()} finite points: bitwise {np.mean(v[both] == ref[both]):.3f}, '
+          f'relative error median {np.median(rel):.2e}, 99th percentile {np.quantile(rel, 0.99):.2e}, max {rel.max():.2e}')
+    # measured: bitwise 0.343, median 1.8e-16, p99 1.5e-7, max 4.1e-7 -- the large
+    # ones at -LML ~ 2e10, kernels so ill-conditioned (jitter 1e-20) that cond(K) * 1e-16 is ~1e-7
+    assert np.mean(v[both] == ref[both]) >= 0.30
+    assert rel.max() < 1e-6 and np.quantile(rel, 0.99) < 5e-7
+    assert np.median(rel) < 1e-15
 
 
 def test_nlml_singular_kernel_failure_semantics():
@@ -133,7 +138,10 @@ def test_nlml_singular_kernel_failure_semantics():
     v = np.array([[O.nlml(D2, L['yd'][:, 0], th, jit) for th in L['thetas']] for jit in L['jitters']])
     ref = L['nlml_dup']
     agree = (np.isinf(v) == np.isinf(ref)).mean()
-    assert agree > 0.99          # pass/fail flips only at the numerical edge of positive-definiteness
+    print(f'Cholesky pass/fail vs the reference on duplicated rows: {agree:.4f} '
+          f'({(np.isinf(v) != np.isinf(ref)).sum()} flips of {v.size})')
+    # measured: 2 flips of 1089 (0.9982), both at the numerical edge of positive-definiteness
+    assert agree >= 0.997
     both = np.isfinite(v) & np.isfinite(ref)
     rel = np.abs(v[both] - ref[both]) / np.maximum(1, np.abs(ref[both]))
     assert np.median(rel) < 1e-10
@@ -194,17 +202,23 @@ def test_nelder_mead_logic_bit_exact_vs_scipy(maxfev):
 
 
 def test_nm_fits_track_reference():
-    """Full fits on the reference -LML.  Per-fit iterates are NOT pinned (roundoff in the
-    -LML redirects NM in flat directions); the optimum value mostly agrees."""
+    """Full fits on the reference -LML.  Per-fit iterates are NOT bitwise the reference's: the
+    oracle's exp / 10^x / log and its sum orders differ from numpy's in the last ulp, which
+    redirects Nelder-Mead in flat directions (tools/fit_agreement.py attributes every mismatch:
+    profiles/r05/fit_agreement.txt); the optimum value agrees.  Measured: 80 of 81
+    optimum values within 1e-6, 21 of 81 fits bitwise."""
     N = golden('nm.npz')
-    agree = []
+    agree, bitwise = [], []
     for tag in ['m10', 'm18tol3', 'm30']:
         xm, ym, ins, th0, tol, out = [N[tag + '__' + k] for k in ['xm', 'ym', 'ins', 'th0', 'tol', 'out']]
         D2 = O.d2_matrix(xm)
         for q, (j, jit) in enumerate(ins):
             th, fv, ne = O.nm_fit(D2, ym[:, int(j)], th0[q], jit, tol[0], tol[1])
             agree.append(abs(fv - out[q, 2]) <= 1e-6 * max(1, abs(out[q, 2])))
-    assert np.mean(agree) > 0.9
+            bitwise.append(np.array_equal(th, out[q, :2]) and fv == out[q, 2])
+    print(f'NM fits vs the reference: optimum within 1e-6 {sum(agree)}/{len(agree)}, '
+          f'bitwise {sum(bitwise)}/{len(bitwise)}')
+    assert sum(agree) >= len(agree) - 3 and sum(bitwise) >= 15
 
 
 def test_knn_matches_reference_up_to_exact_ties():
@@ -230,10 +244,17 @@ def test_predict_d128_matches_reference():
     ref = P['preds']
     scale = np.max(np.abs(ref))
     close = np.abs(preds - ref) <= 1e-8 * scale
-    # a coordinate whose best (jitter, restart) fit flips on roundoff moves by O(1e-2) of scale
-    assert close.mean() >= 0.97 and np.max(np.abs(preds - ref)) <= 5e-2 * scale
     r = P['fit_res']
-    assert np.mean(np.abs(fits[:, 2] - r[:, 2]) <= 1e-6 * np.maximum(1, np.abs(r[:, 2]))) > 0.9
+    fclose = np.abs(fits[:, 2] - r[:, 2]) <= 1e-6 * np.maximum(1, np.abs(r[:, 2]))
+    print(f'predictions within 1e-8 of scale: {close.sum()}/128, max {np.max(np.abs(preds - ref)) / scale:.2e} of '
+          f'scale; fit optima within 1e-6: {fclose.sum()}/1152')
+    # measured (profiles/r05/fit_agreement.txt): 127 of 128 predictions within 1e-8 of the scale,
+    # the other (coordinate 5: the same arg-min jitter, an optimum elsewhere inside the 0.1
+    # tolerance) 2.0e-5 of it; 1 096 of 1 152 optima within 1e-6 -- the other 56 are fits that
+    # stopped elsewhere inside xatol / fatol = 0.1 after an ulp-level difference in exp / 10^x
+    # (53 % of all path differences) or in log and the sum orders (44 %)
+    assert close.sum() >= 126 and np.max(np.abs(preds - ref)) <= 1e-4 * scale
+    assert fclose.sum() >= 1070
 
 
 # --------------------------------------------------------------------------------------------
