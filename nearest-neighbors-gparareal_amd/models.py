@@ -334,6 +334,30 @@ def _select_fit(theta, fval, jitter):
     return tuple(float(v) for v in theta[best]), float(fval[best]), float(jitter[best])
 
 
+def _group_world(group):
+    """(world, rank) of a torch.distributed group, (1, 0) without one."""
+    import torch.distributed as dist
+    if group is False or not (dist.is_available() and dist.is_initialized()):
+        return 1, 0
+    return dist.get_world_size(group), dist.get_rank(group)
+
+
+def _gather_rows(local, group, world):
+    """All-gather of equal [chunk][...] fp64 blocks in rank order over `group`: RCCL's
+    all_gather_into_tensor on device tensors (an NCCL group), gloo's list form through host memory
+    (several ranks sharing one GPU)."""
+    import torch
+    import torch.distributed as dist
+    if dist.get_backend(group) == 'gloo':
+        host = local.detach().cpu()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host, group=group)
+        return torch.cat(parts).to(local.device)
+    out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, local.contiguous(), group=group)
+    return out
+
+
 class GPjax_p(ModelAbstr):
     """Full-data GParareal correction (models.py:273-473) on the GPU.
 
@@ -366,6 +390,11 @@ class GPjax_p(ModelAbstr):
         self.k = 0
         self.rounds = []
         self._dev = None   # (X [rows][n], alpha [n][rows], coef [n][2]) device tensors
+        # multi-GPU (the reference's pool.map over the d*9 fits, models.py:386-392):
+        # the torch.distributed group the fits are sharded over by coordinate (Parareal sets it;
+        # None = the default group when one is initialised, False = never shard)
+        self.process_group = kwargs.get('process_group')
+        self.shard_fits = kwargs.get('shard_fits', True)
 
     def get_times(self):
         out = super().get_times()
@@ -409,11 +438,41 @@ class GPjax_p(ModelAbstr):
             opt_params, opt_fval, opt_jitter = self._train_coord_rnd(X, Y, coord)
         return opt_params, opt_fval, opt_jitter
 
+    def _shard(self):
+        """(group, world, rank, c0, c1, chunk) of the coordinate split, or None on one rank."""
+        if not self.shard_fits:
+            return None
+        world, rank = _group_world(self.process_group)
+        if world <= 1:
+            return None
+        chunk = (self.n + world - 1) // world
+        c0, c1 = min(rank * chunk, self.n), min((rank + 1) * chunk, self.n)
+        return self.process_group, world, rank, c0, c1, chunk
+
     def _train(self, X, Y, old_thetas):
-        """models.py:376-417: every (coordinate, jitter) fit from the coordinate's old theta."""
-        ins = list(product(range(self.n), JITTERS))
-        th, fv, _ = self._fit_batch(X, Y, [i[0] for i in ins], [i[1] for i in ins],
-                                    [old_thetas[i[0]] for i in ins])
+        """models.py:376-417: every (coordinate, jitter) fit from the coordinate's old theta.
+        Over several ranks each fits its own contiguous block of coordinates (every fit's
+        arithmetic is independent of which others share its batch), then ONE all-gather of
+        (theta, fval, nfev) gives every rank all fits; the selection, the random-restart fallback
+        (whose draws come from the shared rng stream) and the weights stay replicated."""
+        nj = len(JITTERS)
+        sh = self._shard()
+        if sh is None:
+            ins = list(product(range(self.n), JITTERS))
+            th, fv, _ = self._fit_batch(X, Y, [i[0] for i in ins], [i[1] for i in ins],
+                                        [old_thetas[i[0]] for i in ins])
+        else:
+            import torch
+            group, world, rank, c0, c1, chunk = sh
+            buf = torch.zeros((chunk * nj, 4), dtype=torch.float64, device=X.device)
+            if c1 > c0:
+                ins = list(product(range(c0, c1), JITTERS))
+                th_l, fv_l, ne_l = self._fit_batch(X, Y, [i[0] for i in ins], [i[1] for i in ins],
+                                                   [old_thetas[i[0]] for i in ins])
+                buf[:len(ins)] = torch.tensor(np.column_stack([th_l, fv_l, ne_l]), dtype=torch.float64)
+            allf = _gather_rows(buf, group, world).cpu().numpy()[:self.n * nj]
+            th, fv = np.ascontiguousarray(allf[:, :2]), np.ascontiguousarray(allf[:, 2])
+            self.train_count[min(self.k, self.N - 1)] += self.n * nj - (c1 - c0) * nj   # all fits, as one rank counts them
         temp = np.zeros((self.n, len(self.theta)))
         nj = len(JITTERS)
         for j in range(self.n):
@@ -434,15 +493,33 @@ class GPjax_p(ModelAbstr):
         (reproduced)."""
         import torch
         n, rows = self.n, X.shape[0]
-        alpha = torch.empty((n, rows), dtype=torch.float64, device=X.device)
-        th, tp = _lib.host_doubles(np.array(self.thetas, dtype=float))
-        jx, jp = _lib.host_doubles(np.array(self.jitters, dtype=float))
-        c = np.arange(n, dtype=np.int32)
-        fv = np.empty(n)
         ip = ctypes.POINTER(ctypes.c_int32)
-        _lib.check(_lib.lib().nngp_gpfull_lml(
-            X.data_ptr(), rows, n, Y.data_ptr(), n, c.ctypes.data_as(ip), jp, tp, fv.ctypes.data_as(_lib._dp),
-            alpha.data_ptr(), torch.cuda.current_stream().cuda_stream))
+
+        def lml(c0, c1, alpha_out):
+            th, tp = _lib.host_doubles(np.array(self.thetas[c0:c1], dtype=float))
+            jx, jp = _lib.host_doubles(np.array(self.jitters[c0:c1], dtype=float))
+            c = np.arange(c0, c1, dtype=np.int32)
+            fv = np.empty(c1 - c0)
+            _lib.check(_lib.lib().nngp_gpfull_lml(
+                X.data_ptr(), rows, n, Y.data_ptr(), c1 - c0, c.ctypes.data_as(ip), jp, tp,
+                fv.ctypes.data_as(_lib._dp), alpha_out.data_ptr(), torch.cuda.current_stream().cuda_stream))
+            return fv
+
+        sh = self._shard()
+        if sh is None:
+            alpha = torch.empty((n, rows), dtype=torch.float64, device=X.device)
+            fv = lml(0, n, alpha)
+        else:   # each rank its coordinates' weights, then one all-gather of [chunk][rows] (+ fval)
+            group, world, rank, c0, c1, chunk = sh
+            buf = torch.zeros((chunk, rows + 1), dtype=torch.float64, device=X.device)
+            if c1 > c0:
+                part = torch.empty((c1 - c0, rows), dtype=torch.float64, device=X.device)
+                fv_l = lml(c0, c1, part)
+                buf[:c1 - c0, 1:] = part
+                buf[:c1 - c0, 0] = torch.tensor(fv_l, dtype=torch.float64)
+            allb = _gather_rows(buf, group, world)[:n]
+            alpha = allb[:, 1:].contiguous()
+            fv = allb[:, 0].cpu().numpy()
         if np.any(np.isinf(fv)):
             raise np.linalg.LinAlgError('Matrix is not positive definite')   # np.linalg.cholesky in _predict
         first = {}

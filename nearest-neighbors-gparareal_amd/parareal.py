@@ -248,6 +248,8 @@ class Parareal():
                               f'raises if it gets there (pass early_stop <= {MAX_NEIGHBOURS - 1} or a fixed nn)')
         elif model.lower() == 'gpjax':
             mdl = GPjax_p(n=self.n, N=self.N, worker_pool=kwargs['pool'], **kwargs)
+            if 'process_group' not in kwargs:
+                mdl.process_group = self.process_group   # the fits shard over the driver's group
         elif model.lower() == 'elm':
             raise NotImplementedError(f'model {model!r} is outside the GParareal/nnGP path (SURVEY.md §7)')
         else:

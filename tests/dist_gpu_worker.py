@@ -37,6 +37,11 @@ def run_case(g, case, shard, native=None):
         s = g.SolverRK(ode.get_vector_field(), Ng=50, Nf=195325, F='RK8', G='RK4', thresh=float('inf'))
         p = g.Parareal(ode, s, [0, 1100], 512, epsilon=5e-7, verbose=None)
         kw = dict(model='nngp', nn=20, seed=45, early_stop=1)
+    elif case == 'gp_burgers':   # GParareal (full-data GP): its d*9 = 576 fits sharded by coordinate
+        ode = g.Burgers(d_x=64, normalization='-11')
+        s = g.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
+        p = g.Parareal(ode, s, [0, 1.25], 16, epsilon=5e-7, verbose=None)
+        kw = dict(model='gpjax', early_stop=3)
     else:                   # classic Parareal on Lorenz (BASELINE configs[0]'s schedule)
         ode = g.Lorenz(normalization='-11')
         s = g.SolverRK(ode.get_vector_field(), Ng=6, Nf=450, F='RK4', G='RK4')

@@ -26,10 +26,13 @@ def _port():
 
 @pytest.mark.timeout(400)
 @pytest.mark.parametrize('case,shard,world', [('lorenz', 'none', 2), ('burgers', 'none', 2), ('burgers', '1', 3),
-                                              ('fhn', '1', 2), ('tomlab256', 'none', 8), ('fhn800', '1', 8)])
+                                              ('fhn', '1', 2), ('tomlab256', 'none', 8), ('fhn800', '1', 8),
+                                              ('gp_burgers', 'none', 2), ('gp_burgers', 'none', 3)])
 def test_multi_rank_gpu_run_equals_single_rank(gpu, case, shard, world, tmp_path):
     """world 8: BASELINE configs[3] / configs[4]'s 8-way partitions (TomLab N=256: 32 slices per
-    rank; FHN-PDE d=800 N=512: 64 slices and 100 of the 800 coordinates per rank)."""
+    rank; FHN-PDE d=800 N=512: 64 slices and 100 of the 800 coordinates per rank).  gp_burgers:
+    GParareal's d*9 = 576 fits and its 64 posterior-weight vectors sharded by coordinate (32 / 32
+    and 22 / 22 / 20 per rank), one all-gather each per iteration (models.GPjax_p._train/_weights)."""
     k1, conv1, u1 = run_case(gpu, case, None if shard == 'none' else shard == '1')
     out = str(tmp_path / 'rank0.npz')
     port = _port()
