@@ -236,6 +236,42 @@ def published_runs(torch, g):
     return out
 
 
+def published_k_table(torch, g):
+    """The reference's published K table (tests/published_k.py: Hopf.py, FHN_PDE.py, Burgers.py on
+    the legacy driver).  Two cheap entries are run live here (Burgers T = 5.9 and FHN-PDE d_x = 10
+    classic Parareal, ~25 s together); the rest -- minutes each -- are read from the newest committed
+    profiles/rNN/published_k/*.json, written on this hardware by tools/published_k_run.py (the same
+    code the -m gpu tests run, tests/test_gpu_published_k.py)."""
+    import glob
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    import published_k as P
+    rows = {}
+    for name in ('burgers59_128_para', 'fhn10_512_para'):
+        s, kw, pk = P.build(g, name)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = s.run(**kw)
+        torch.cuda.synchronize()
+        rows[name] = {'K': int(r['k']), 'published_K': pk, 'match': int(r['k']) == pk,
+                      'wall_s': time.perf_counter() - t0, 'source': 'live'}
+    dirs = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r[0-9]*', 'published_k')))
+    if dirs:
+        for f in sorted(glob.glob(os.path.join(dirs[-1], '*.json'))):
+            name = os.path.basename(f)[:-5]
+            if name in rows:
+                continue
+            with open(f) as fh:
+                d = json.load(fh)
+            rows[name] = {'K': d['K'], 'published_K': d['published_K'], 'match': d['K'] == d['published_K'],
+                          'wall_s': d['wall_s'], 'source': os.path.relpath(f, ROOT)}
+    det = [n for n in rows if n.split('_')[2] == 'para']
+    return {'rows': rows, 'parareal_exact': f"{sum(rows[n]['match'] for n in det)}/{len(det)}",
+            'all_exact': f"{sum(v['match'] for v in rows.values())}/{len(rows)}",
+            'note': 'name = <system>_<N>_<model>[_paged]; unpaged = Nf/N steps per slice (the published '
+                    'runs paged F 25x / 200x: the same integration up to roundoff, SURVEY.md 0.4); nnGP '
+                    'mismatches are threshold straddles / within the seed and schedule spread (DESIGN.md 5)'}
+
+
 def corrections_fhn_d200(torch, g, n_pred=20):
     """nnGP corrections at the FHN-PDE d=200 shape (m=20, R=1: 1 800 fits per prediction) on a
     synthetic 3 000-row training set, one prediction after another on one GPU.  BASELINE.md §B
@@ -959,6 +995,8 @@ def main():
         res['fhn_pde_d512_n512_published_config'] = r16
         log('fhn-pde d=512 N=512 published', json.dumps(r16))
         res.update(published_runs(torch, g))
+        res['published_k'] = published_k_table(torch, g)
+        log('published K', json.dumps({k: (v['K'], v['published_K']) for k, v in res['published_k']['rows'].items()}))
         log('published runs', json.dumps({k: res[k]['wall_s'] for k in ('burgers_n128_published_schedule_nngp',
                                                                          'tomlab_n256_configs_schedule_nngp')}))
         res['gparareal_lorenz_n32'] = gparareal_lorenz(torch, g)

@@ -1,0 +1,131 @@
+"""The reference's published K table (VERDICT.md round 4 "Next round" 1)
+run at the published configurations on the legacy new_lib driver surface (nngp_amd.legacy) --
+tests/published_k.py builds each one from its script (Hopf.py, FHN_PDE.py, Burgers.py), file:line
+cited there, including why an unpaged F is the same integration as the scripts' paged one up to
+roundoff.
+
+Every deterministic classic-Parareal K is asserted EXACTLY equal to the published one.  nnGParareal
+K follows fits that Nelder-Mead steers from the last bits of the GP arithmetic (SURVEY.md §0.6-0.7:
+the reference's own K moves over seeds and under one-ulp perturbations), so an nnGP K that differs
+from the published run is asserted as what it is -- a threshold straddle (the published iteration
+sits just on the other side of epsilon) or a K inside the spread the same configuration shows over
+RNG seeds and over the fine schedule (paged / unpaged) -- with the numbers printed.
+
+Default (the round-end suite, ~3.5 min): Parareal FHN-PDE d_x = 10 / 12 / 16 and Burgers T = 5.9,
+nnGParareal Hopf N = 512 and Burgers T = 5.9 over seeds 45-50, GParareal Burgers T = 5.9.
+NNGP_PUBLISHED=1 adds the long ones (Hopf N = 128 / 512 Parareal, Hopf N = 32 / 128 nnGP and
+GParareal, the paged FHN-PDE and Burgers nnGP runs, FHN-PDE d_x = 10's seeds): ~40 min on one
+MI355X; their results as run for this round are in profiles/r05/published_k/*.json
+(tools/published_k_run.py) and DESIGN.md §5."""
+import os
+
+import numpy as np
+import pytest
+
+from published_k import PUBLISHED_K, build, summarise
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+LONG = pytest.mark.skipif(os.environ.get('NNGP_PUBLISHED') != '1',
+                          reason='set NNGP_PUBLISHED=1 (minutes each; results in profiles/r05/published_k)')
+EPS = 5e-7
+
+
+def _run(gpu, name, **over):
+    s, kw, pk = build(gpu, name)
+    kw.update(over)
+    r = s.run(**kw)
+    out = summarise(r)
+    print(f"{name}: K={out['K']} (published {pk}) conv_int[-6:]={out['conv_int'][-6:]} "
+          f"err_max[-4:]={[f'{e:.3g}' for e in out['err_max'][-4:]]} runtime={out['runtime_s']:.1f}s")
+    return out, pk
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize('name', ['burgers59_128_para', 'fhn10_512_para', 'fhn12_512_para', 'fhn16_512_para'])
+def test_published_parareal_k_exact(gpu, name):
+    """Classic Parareal (no model randomness): K equals the published K exactly --
+    Burgers T=5.9 90, FHN-PDE d_x=10 25, d_x=12 67, d_x=16 79."""
+    out, pk = _run(gpu, name)
+    assert out['converged'] and out['K'] == pk
+
+
+@pytest.mark.timeout(300)
+def test_published_hopf_n512_nngp_k_exact(gpu):
+    """Hopf.py N = 512 nnGParareal (RK8 x 3.4e6 steps/slice, nn=15, R=2, tol 0.1, seed 45): K = 19."""
+    out, pk = _run(gpu, 'hopf_512_nngp')
+    assert out['converged'] and out['K'] == pk == 19
+
+
+@pytest.mark.timeout(300)
+def test_published_burgers59_gparareal_k_exact(gpu):
+    """Burgers.py T = 5.9 GParareal (full-data GP, published K = 8)."""
+    out, pk = _run(gpu, 'burgers59_128_gp')
+    assert out['converged'] and out['K'] == pk == 8
+
+
+@pytest.mark.timeout(300)
+def test_published_burgers59_nngp_straddle_over_seeds(gpu):
+    """Burgers.py T = 5.9 nnGParareal (nn = 18; published K = 14, seed 45).  Here the error maxima
+    decay slowly through iterations 11-16 (a plateau of 5e-7 .. 1e-6 around epsilon = 5e-7), and
+    at the published run's last iteration, 14, EVERY seed 45-50 sits just above epsilon (1.03 to
+    1.6 epsilon: 5.13e-7 for seed 45), so they need one to three more iterations: K = 15, 16, 15, 16,
+    17, 15.  The published run's iteration-14 maximum fell just below epsilon -- a threshold
+    straddle on a plateau, which the last-ulp differences of the GP arithmetic (XLA / OpenBLAS
+    against the restatement) decide.  (The published 200-page schedule: K = 16,
+    6.85e-7 at iteration 14; test_published_burgers59_nngp_paged.)"""
+    ks, e14 = {}, {}
+    for seed in (45, 46, 47, 48, 49, 50):
+        o, pk = _run(gpu, 'burgers59_128_nngp', seed=seed)
+        assert o['converged'] and pk == 14
+        ks[seed], e14[seed] = o['K'], o['err_max'][13]
+    print('Burgers T=5.9 nnGP K over seeds:', ks, 'iteration-14 error maxima:', e14)
+    assert ks[45] == 15 and EPS < e14[45] < 1.1 * EPS
+    assert all(15 <= k <= 17 for k in ks.values())
+    assert all(EPS < e < 1.6 * EPS for e in e14.values())
+
+
+# --------------------------------------------------------------------------------- long (opt-in)
+@LONG
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize('name', ['hopf_512_para', 'hopf_128_para'])
+def test_published_hopf_parareal_k_exact(gpu, name):
+    """Hopf.py Parareal N = 512 (K = 149, 276 s) and N = 128 (K = 54, 430 s)."""
+    out, pk = _run(gpu, name)
+    assert out['converged'] and out['K'] == pk
+
+
+@LONG
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('name', ['hopf_128_nngp', 'hopf_128_gp', 'hopf_32_nngp', 'hopf_32_gp',
+                                  'fhn12_512_nngp_paged'])
+def test_published_model_k_exact(gpu, name):
+    """Hopf N = 128 nnGParareal (K = 13) and GParareal (theta [1, 1], tol 1e-6: K = 16), Hopf N = 32
+    nnGParareal (K = 9) and GParareal (K = 10), and FHN-PDE d_x = 12 nnGParareal on the published
+    paged schedule (K = 10; unpaged it converges in 8)."""
+    out, pk = _run(gpu, name)
+    assert out['converged'] and out['K'] == pk
+
+
+@LONG
+@pytest.mark.timeout(900)
+def test_published_fhn10_nngp_within_schedule_and_seed_spread(gpu):
+    """FHN-PDE d_x = 10 nnGParareal (published K = 12): K = 11 on the published paged schedule, its
+    iterations 9 and 10 at 1.38 and 1.24 epsilon before it converges; unpaged (the same steps per
+    slice but 25 times coarser) every seed 45-49 gives K = 9 -- the fine schedule alone moves K by 2."""
+    out, pk = _run(gpu, 'fhn10_512_nngp_paged')
+    assert out['converged'] and abs(out['K'] - pk) <= 1
+    ks = {}
+    for seed in (45, 46, 47, 48, 49):
+        o, _ = _run(gpu, 'fhn10_512_nngp', seed=seed)
+        ks[seed] = o['K']
+    print('FHN-PDE d_x=10 nnGP (unpaged) K over seeds:', ks, 'paged seed 45:', out['K'], 'published', pk)
+    assert set(ks.values()) == {9}
+
+
+@LONG
+@pytest.mark.timeout(900)
+def test_published_burgers59_nngp_paged(gpu):
+    """Burgers T = 5.9 nnGParareal on the published 200-page schedule: K within 2 of the published 14
+    (16: iterations 14 and 15 at 1.37 and 1.15 epsilon)."""
+    out, pk = _run(gpu, 'burgers59_128_nngp_paged')
+    assert out['converged'] and abs(out['K'] - pk) <= 2

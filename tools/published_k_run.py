@@ -3,6 +3,7 @@ K, conv_int, the per-iteration error maxima and timings, one JSON file per entry
 gpurun_out/published_k/ (copied to profiles/r05/ afterwards).
 
     python -u tools/published_k_run.py fhn10_512_para fhn10_512_nngp hopf_512_nngp ...
+    python -u tools/published_k_run.py burgers59_128_nngp@46 ...     (another RNG seed; file name@46.json)
 
 Progress goes to stdout every iteration (verbose driver), so a long entry is never silent."""
 import json
@@ -22,17 +23,20 @@ def main(names):
     torch.cuda.set_device(0)
     out_dir = os.path.join(ROOT, 'gpurun_out', 'published_k')
     os.makedirs(out_dir, exist_ok=True)
-    for name in names:
+    for tag in names:
+        name, _, seed = tag.partition('@')
         s, kw, pk = P.build(gpu, name, verbose='v')
+        if seed:
+            kw['seed'] = int(seed)
         print(f'=== {name}: published K {pk}; run kwargs {kw}; Nf/N {s.Nf // s.N}, RK_thresh {s.RK_thresh}',
               flush=True)
         t0 = time.time()
         r = s.run(**kw)
         summ = P.summarise(r)
-        summ.update(name=name, published_K=pk, wall_s=time.time() - t0, Nf_per_slice=s.Nf // s.N,
+        summ.update(name=tag, published_K=pk, wall_s=time.time() - t0, Nf_per_slice=s.Nf // s.N,
                     Ng_per_slice=s.Ng // s.N, RK_thresh=s.RK_thresh, run_kwargs={k: v for k, v in kw.items()},
                     spec_hits=r['timings'].get('spec_hits'))
-        with open(os.path.join(out_dir, name + '.json'), 'w') as f:
+        with open(os.path.join(out_dir, tag + '.json'), 'w') as f:
             json.dump(summ, f, indent=1)
         print('RESULT', json.dumps(summ), flush=True)
 
