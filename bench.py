@@ -258,7 +258,7 @@ def published_k_table(torch, g):
     if dirs:
         for f in sorted(glob.glob(os.path.join(dirs[-1], '*.json'))):
             name = os.path.basename(f)[:-5]
-            if name in rows:
+            if name in rows or '@' in name:   # name@seed: the seed-spread runs
                 continue
             with open(f) as fh:
                 d = json.load(fh)
@@ -267,9 +267,10 @@ def published_k_table(torch, g):
     det = [n for n in rows if n.split('_')[2] == 'para']
     return {'rows': rows, 'parareal_exact': f"{sum(rows[n]['match'] for n in det)}/{len(det)}",
             'all_exact': f"{sum(v['match'] for v in rows.values())}/{len(rows)}",
-            'note': 'name = <system>_<N>_<model>[_paged]; unpaged = Nf/N steps per slice (the published '
-                    'runs paged F 25x / 200x: the same integration up to roundoff, SURVEY.md 0.4); nnGP '
-                    'mismatches are threshold straddles / within the seed and schedule spread (DESIGN.md 5)'}
+            'note': 'name = <system>_<N>_<model>[_paged]; unpaged = Nf/N RK steps per slice; the published '
+                    'runs paged F (RK_thresh: every one of 25 / 200 pages re-uses all Nf/N steps), the same '
+                    'solution to roundoff (SURVEY.md 0.4); nnGP mismatches are epsilon straddles or within '
+                    'the seed / schedule spread (DESIGN.md 5)'}
 
 
 def corrections_fhn_d200(torch, g, n_pred=20):

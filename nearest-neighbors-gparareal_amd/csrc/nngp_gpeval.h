@@ -201,7 +201,7 @@ __device__ __forceinline__ bool gp_factor(int m, int l, const GPLane<MAXM> &P, c
                 if (j >= 16 * (s + 1)) continue;
                 double e = (row >= m && j == row) ? 1.0 : 0.0;
                 if (row < m && j <= row) {
-                    e = psy * nn_exp_nonpos(c * sD2[row * m + j]);
+                    e = psy * nn_exp_nonpos_sep(c * sD2[row * m + j]);
                     if (j == row) e = e + jit;
                 }
                 a[s][j] = e;
@@ -453,7 +453,8 @@ __device__ __forceinline__ double gp_mean(int m, int l, const GPLane<MAXM> &P, c
 #pragma unroll
     for (int s = 0; s < RPL; s++) {
         const int row = l + 16 * s;
-        ka[s] = (psy * nn_exp_nonpos(c * skd2[row < m ? row : 0])) * alpha[s];
+        const double x = c * skd2[row < m ? row : 0];
+        ka[s] = (psy * (GP<MAXM>::BIG ? nn_exp_nonpos_sep(x) : nn_exp_nonpos(x))) * alpha[s];
     }
     const double mean = gp_rows_sum<RPL>(m, l, ka);
     return ok ? mean : NAN;

@@ -42,25 +42,39 @@ __device__ __forceinline__ double fma3(double a, double b, double c) {
 // the same bits with three ops fewer: the upper clamp and the overflow select are never taken
 // there, and r + 0 only normalises the sign of a zero r, which no term of the polynomial sees
 // (p = fma(p, +-0, c) = c).
-template <bool NONPOS = false>
+// BLOCK: the Horner steps as one asm block (below); false keeps ten separate fma3 statements,
+// which the register-starved m > 32 fit kernels schedule better (fewer spills).
+template <bool NONPOS = false, bool BLOCK = true>
 __device__ __forceinline__ double nn_exp_t(double hi, double lo) {
     const double xc = NONPOS ? fmax(hi, -746.0) : fmin(fmax(hi, -746.0), 710.0);   // NaN -> -746
     const double n = rint(xc * MathC::INV_LN2);
     double r = fma(-n, MathC::LN2_HI, xc);
     r = fma(-n, MathC::LN2_LO, r);
     if constexpr (!NONPOS) r = r + lo;
-    // sum_{j=0}^{13} r^j / j!
-    double p = 1.0 / 6227020800.0;             // 1/13!
-    p = fma3(p, r, 1.0 / 479001600.0);         // 1/12!
-    p = fma3(p, r, 1.0 / 39916800.0);
-    p = fma3(p, r, 1.0 / 3628800.0);
-    p = fma3(p, r, 1.0 / 362880.0);
-    p = fma3(p, r, 1.0 / 40320.0);
-    p = fma3(p, r, 1.0 / 5040.0);
-    p = fma3(p, r, 1.0 / 720.0);
-    p = fma3(p, r, 1.0 / 120.0);
-    p = fma3(p, r, 1.0 / 24.0);
-    p = fma3(p, r, 1.0 / 6.0);
+    // sum_{j=0}^{13} r^j / j!: the first ten Horner steps (1/13! .. 1/3!) as ONE asm block of
+    // 3-address v_fma_f64 (see fma3; one block instead of ten, because LLVM's hazard recognizer
+    // puts an s_nop after every inline asm statement), then three plain steps
+    double p;
+    if constexpr (!BLOCK) {
+        p = fma3(1.0 / 6227020800.0, r, 1.0 / 479001600.0);
+        p = fma3(p, r, 1.0 / 39916800.0);
+        p = fma3(p, r, 1.0 / 3628800.0);
+        p = fma3(p, r, 1.0 / 362880.0);
+        p = fma3(p, r, 1.0 / 40320.0);
+        p = fma3(p, r, 1.0 / 5040.0);
+        p = fma3(p, r, 1.0 / 720.0);
+        p = fma3(p, r, 1.0 / 120.0);
+        p = fma3(p, r, 1.0 / 24.0);
+        p = fma3(p, r, 1.0 / 6.0);
+    } else
+    asm("v_fma_f64 %0, %2, %1, %3\n\t"
+        "v_fma_f64 %0, %0, %1, %4\n\tv_fma_f64 %0, %0, %1, %5\n\tv_fma_f64 %0, %0, %1, %6\n\t"
+        "v_fma_f64 %0, %0, %1, %7\n\tv_fma_f64 %0, %0, %1, %8\n\tv_fma_f64 %0, %0, %1, %9\n\t"
+        "v_fma_f64 %0, %0, %1, %10\n\tv_fma_f64 %0, %0, %1, %11\n\tv_fma_f64 %0, %0, %1, %12"
+        : "=&v"(p)
+        : "v"(r), "v"(1.0 / 6227020800.0), "v"(1.0 / 479001600.0), "v"(1.0 / 39916800.0),
+          "v"(1.0 / 3628800.0), "v"(1.0 / 362880.0), "v"(1.0 / 40320.0), "v"(1.0 / 5040.0),
+          "v"(1.0 / 720.0), "v"(1.0 / 120.0), "v"(1.0 / 24.0), "v"(1.0 / 6.0));
     p = fma(p, r, 0.5);
     p = fma(p, r, 1.0);
     p = fma(p, r, 1.0);
@@ -74,6 +88,7 @@ __device__ __forceinline__ double nn_exp_dd(double hi, double lo) { return nn_ex
 __device__ __forceinline__ double nn_exp(double x) { return nn_exp_t<false>(x, 0.0); }
 // exp(x) for x <= 0 or NaN only (see NONPOS)
 __device__ __forceinline__ double nn_exp_nonpos(double x) { return nn_exp_t<true>(x, 0.0); }
+__device__ __forceinline__ double nn_exp_nonpos_sep(double x) { return nn_exp_t<true, false>(x, 0.0); }
 
 // sqrt(x) and 1.0/x, correctly rounded, for x in [2^-500, 2^500]: the instruction sequences the
 // compiler emits for sqrt() and 1.0/x on gfx950 (rsq + Goldschmidt with two corrections; rcp +

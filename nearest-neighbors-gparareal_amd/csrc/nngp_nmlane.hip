@@ -58,6 +58,43 @@ __device__ __forceinline__ T gbcast(T v) {
     }
 }
 
+// gbcast of a double as ONE volatile asm (two v_mov_b32_dpp, s_nop 1 first for the DPP read
+// hazard), which also takes two values of the previous k's updates (dep0, dep1; unused): the
+// broadcast of x_k then waits for them, so at most one or two x's are live -- left free, LLVM
+// computed every column's broadcasts up front (~34 broadcast doubles live at M = 15's peak)
+template <int LPF, int SRC>
+__device__ __forceinline__ double gbcast_pinned(double v, double dep0, double dep1) {
+    constexpr int Q0 = SRC, Q2 = LPF == 4 ? SRC : 2 + SRC;
+    static_assert(Q0 < 4 && Q2 < 4, "quad lane");
+    uint32_t lo = (uint32_t)__double_as_longlong(v), hi = (uint32_t)(__double_as_longlong(v) >> 32);
+    uint32_t olo, ohi;
+    if constexpr (Q0 == 0 && Q2 == 0)
+        asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %2 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t"
+                     "v_mov_b32_dpp %1, %3 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf"
+                     : "=&v"(olo), "=&v"(ohi) : "v"(lo), "v"(hi), "v"(dep0), "v"(dep1));
+    else if constexpr (Q0 == 1 && Q2 == 1)
+        asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %2 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t"
+                     "v_mov_b32_dpp %1, %3 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf"
+                     : "=&v"(olo), "=&v"(ohi) : "v"(lo), "v"(hi), "v"(dep0), "v"(dep1));
+    else if constexpr (Q0 == 2 && Q2 == 2)
+        asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %2 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf\n\t"
+                     "v_mov_b32_dpp %1, %3 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf"
+                     : "=&v"(olo), "=&v"(ohi) : "v"(lo), "v"(hi), "v"(dep0), "v"(dep1));
+    else if constexpr (Q0 == 3 && Q2 == 3)
+        asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %2 quad_perm:[3,3,3,3] row_mask:0xf bank_mask:0xf\n\t"
+                     "v_mov_b32_dpp %1, %3 quad_perm:[3,3,3,3] row_mask:0xf bank_mask:0xf"
+                     : "=&v"(olo), "=&v"(ohi) : "v"(lo), "v"(hi), "v"(dep0), "v"(dep1));
+    else if constexpr (Q0 == 0)
+        asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %2 quad_perm:[0,0,2,2] row_mask:0xf bank_mask:0xf\n\t"
+                     "v_mov_b32_dpp %1, %3 quad_perm:[0,0,2,2] row_mask:0xf bank_mask:0xf"
+                     : "=&v"(olo), "=&v"(ohi) : "v"(lo), "v"(hi), "v"(dep0), "v"(dep1));
+    else
+        asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %2 quad_perm:[1,1,3,3] row_mask:0xf bank_mask:0xf\n\t"
+                     "v_mov_b32_dpp %1, %3 quad_perm:[1,1,3,3] row_mask:0xf bank_mask:0xf"
+                     : "=&v"(olo), "=&v"(ohi) : "v"(lo), "v"(hi), "v"(dep0), "v"(dep1));
+    return __longlong_as_double((long long)(((uint64_t)ohi << 32) | olo));
+}
+
 // xor partner inside the group: 1 -> quad_perm [1,0,3,2], 2 -> [2,3,0,1]
 template <int X>
 __device__ __forceinline__ double xor_dpp(double v) {
@@ -80,9 +117,12 @@ __device__ __forceinline__ void sqrt_rcp_exact(double x, double &ljj, double &ri
     const int k = x < 0x1p-500 ? 300 : (x > 0x1p+500 ? -300 : 0);
     const double s = sqrt_mid(ldexp(x, 2 * k));
     const double r = rcp_mid(s);
-    const bool inf = x == __builtin_huge_val();
-    ljj = inf ? x : ldexp(s, -k);
-    ri = inf ? 0.0 : ldexp(r, k);
+    // +inf -> (inf, 0) by bit masks, not a select: LLVM turned the select into a branch around the
+    // whole sequence (a divergent branch per column, values spilled across it)
+    const long long m = -(long long)(x == __builtin_huge_val());   // all ones for +inf
+    const long long ls = __double_as_longlong(ldexp(s, -k)), lr = __double_as_longlong(ldexp(r, k));
+    ljj = __longlong_as_double((ls & ~m) | (0x7FF0000000000000ll & m));
+    ri = __longlong_as_double(lr & ~m);
 }
 
 // oracle butterfly_sum over the fit's rows r < M of v[r] (row r = LPF s + q in slot s of lane q):
@@ -181,7 +221,11 @@ __device__ __forceinline__ double lane_nlml(int q, const double *sD2, double sx,
         }
 #pragma unroll
         for (int k = 0; k < j; k++) {
-            const double xk = gbcast<LPF, QJ>(a[SJ][k]);
+            // (the first broadcast of a column also waits for the previous column's last-slot
+            // result: most of a left-looking column's products do not depend on the column before,
+            // and LLVM otherwise ran columns ahead, holding their partial sums and x's)
+            const double xk = gbcast_pinned<LPF, QJ>(a[SJ][k], (k == 0 && j > 0) ? a[RPL - 1][j > 0 ? j - 1 : 0]
+                                                                                 : bk[RPL - 1], tt[RPL - 1]);
 #pragma unroll
             for (int s = SJ; s < RPL; s++) {
                 const bool vec = LPF * s < TS, tail = LPF * s + LPF - 1 >= TS;
@@ -202,8 +246,11 @@ __device__ __forceinline__ double lane_nlml(int q, const double *sD2, double sx,
             const bool vec = LPF * s < TS, tail = LPF * s + LPF - 1 >= TS;
             double y = vec ? yv[s] : a[s][j] - tt[s];
             if (vec && tail) y = (LPF * s + q < TS) ? yv[s] : a[s][j] - tt[s];
-            // rows <= j of slot SJ keep what they hold (the owner's diagonal K_jj is no longer read)
-            a[s][j] = (s > SJ || q > QJ) ? y * ri : a[s][j];
+            // (rows <= j of slot SJ store garbage here: their entry j is above the diagonal, or --
+            // for row j itself -- the diagonal K_jj, which nothing reads after the pivot; the back
+            // solve's image takes the strictly lower entries only.  A select kept the old values
+            // alive: 64 VGPRs at M = 15.)
+            a[s][j] = y * ri;
         }
         // forward solve, fused: z_j = acc_j / L_jj, then rows below subtract L_ij z_j (models.py:90)
         const double zj = mk_div(gbcast<LPF, QJ>(acc[SJ]), ljj, ri);
@@ -353,11 +400,224 @@ __global__ void __launch_bounds__(256) nm_lane_kernel(NMArgs a) {
     write_fit();
 }
 
-// instantiated neighbour counts: the speculative batches of the BASELINE configs (Burgers nn = 15,
-// Hopf / Lorenz 10-15), four lanes per fit.  (m >= 17 would need more than a lane's 256 VGPRs at
-// LPF = 4 -- the packed kernel serves it.)
-template <int M> struct LaneLPF { static constexpr int V = 4; };
+// ---------------------------------------------------------------------------------------------
+// One fit per lane (LPF = 1): 64 fits per wave, no cross-lane traffic at all.
+//
+// A lane holds its fit's whole lower triangle (M(M+1)/2 doubles, K overwritten in place by L, the
+// diagonal by L_jj) in registers -- more than 256 VGPRs from M = 15 on, so the kernel runs one
+// wave per SIMD with the AGPR half of the register file; a wave's dependent fp64 ops issue as fast
+// as independent ones (tools/ubench_fp64.hip), so one wave keeps the SIMD's VALU busy.  The D^2
+// entries are wave-uniform (a workgroup serves one prediction): LDS reads every lane of a wave
+// makes at the same address (a broadcast, no bank conflicts).  The arithmetic of every
+// entry is lane_nlml's / the oracle's (gp_factor, orc_nlml), only scheduled row by row:
+//   * L_ij, i > j: dpotf2_L's vector-row / tail-row forms, chosen at compile time (M is exact);
+//   * z: acc_i = y_i - L_i0 z_0 - L_i1 z_1 - ... (k ascending), z_i = acc_i / L_ii (Markstein) --
+//     the fused forward solve's order;
+//   * alpha: acc_r = z_r - L_{M-1,r} alpha_{M-1} - ... (i descending), the back solve's order;
+//   * the two sums: the 16-slot butterfly, all levels inside the lane.
+// Issued instructions per fit-evaluation drop ~3x against LPF = 4 (no replicated pivots, no
+// broadcasts, no masked rows, no DPP hazards; tools/nm_lanes_probe.py).
+// ---------------------------------------------------------------------------------------------
+template <int M> struct Lane1 {
+    static constexpr int T = M * (M + 1) / 2;
+    static constexpr int at(int r, int k) { return r * (r + 1) / 2 + k; }
+    static constexpr int tail_start(int j) { return j + 1 + ((M - 1 - j) & ~3); }
+};
 
+// ys: this lane's y column in LDS, row r at ys[r * 256]
+template <int M>
+__device__ __forceinline__ double lane1_nlml(const double *D2, double sx, double sy, double jit, const double *ys) {
+    using LF = Lane1<M>;
+    const double c = -0.5 * (1 / nn_pow10(sx));
+    const double psy = nn_pow10(sy);
+    double a[LF::T];
+    // K_rk = psy exp(c D2_rk) (+ jit on the diagonal), models.py:146-155, 88; the exps as a chain
+    // (see lane_nlml): at most two in flight
+    double e1 = 0.0, e2 = 0.0;
+    static_for<0, M>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        static_for<0, r + 1>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            asm volatile("" ::"v"(e2) : "memory");
+            double e = psy * nn_exp_nonpos(c * D2[r * M + k]);
+            if constexpr (k == r) e = e + jit;
+            a[LF::at(r, k)] = e;
+            e2 = e1;
+            e1 = e;
+        });
+    });
+    bool bad = false;
+    double ri[M];
+    static_for<0, M>([&](auto jc) {
+        constexpr int j = decltype(jc)::value, JB = j & ~3, TS = LF::tail_start(j);
+        // pivot: a_jj - ddot(row j) (potf2_dot)
+        double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+        for (int k = 0; k + 4 <= j; k += 4) {
+            t1 = t1 + fma(a[LF::at(j, k)], a[LF::at(j, k)], a[LF::at(j, k + 2)] * a[LF::at(j, k + 2)]);
+            t2 = t2 + fma(a[LF::at(j, k + 1)], a[LF::at(j, k + 1)], a[LF::at(j, k + 3)] * a[LF::at(j, k + 3)]);
+        }
+#pragma unroll
+        for (int k = JB; k < j; k++) t1 = fma(a[LF::at(j, k)], a[LF::at(j, k)], t1);
+        const double pv = a[LF::at(j, j)] - (t1 + t2);
+        bad = bad || !(pv > 0.0);
+        double ljj, rj;
+        sqrt_rcp_exact(pv, ljj, rj);
+        a[LF::at(j, j)] = ljj;
+        ri[j] = rj;
+        // rows below j: dgemv_n's vector rows (y -= 4-column fma blocks, leftover y -= a x) and
+        // tail rows (y -= one fma chain), then * RN(1/L_jj)
+        static_for<j + 1, M>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            double y;
+            if constexpr (i < TS) {
+                double yv = a[LF::at(i, j)], bk = 0.0;
+#pragma unroll
+                for (int k = 0; k < j; k++) {
+                    const double p = a[LF::at(i, k)], x = a[LF::at(j, k)];
+                    if (k < JB) {
+                        bk = (k % 4 == 0) ? p * x : fma(p, x, bk);
+                        if (k % 4 == 3) yv = yv - bk;
+                    } else {
+                        yv = yv - p * x;
+                    }
+                }
+                y = yv;
+            } else {
+                double tt = 0.0;
+#pragma unroll
+                for (int k = 0; k < j; k++) tt = fma(a[LF::at(i, k)], a[LF::at(j, k)], tt);
+                y = a[LF::at(i, j)] - tt;
+            }
+            a[LF::at(i, j)] = y * rj;
+        });
+    });
+    // forward solve L z = y (models.py:90), row by row in the fused solve's order
+    double z[M];
+    static_for<0, M>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        double acc = ys[i * 256];
+#pragma unroll
+        for (int k = 0; k < i; k++) acc = acc - a[LF::at(i, k)] * z[k];
+        z[i] = mk_div(acc, a[LF::at(i, i)], ri[i]);
+    });
+    // back solve L^T alpha = z, rows descending, each row's terms i descending (alpha over z)
+    static_for<0, M>([&](auto rc) {
+        constexpr int r = M - 1 - decltype(rc)::value;
+        double acc = z[r];
+#pragma unroll
+        for (int i = M - 1; i > r; i--) acc = acc - a[LF::at(i, r)] * z[i];
+        z[r] = mk_div(acc, a[LF::at(r, r)], ri[r]);
+    });
+    // -LML: the oracle's 16-slot butterflies of y_r alpha_r and log L_rr
+    double py[16], pl[16];
+#pragma unroll
+    for (int s = 0; s < 16; s++) {
+        py[s] = s < M ? ys[(s < M ? s : 0) * 256] * z[s < M ? s : 0] : 0.0;
+        pl[s] = s < M ? nn_log(a[LF::at(s < M ? s : 0, s < M ? s : 0)]) : 0.0;
+#pragma unroll
+        for (int f = 1; 16 * f < M; f++) {
+            const int r = s + 16 * f;
+            py[s] = py[s] + (r < M ? ys[(r < M ? r : 0) * 256] * z[r < M ? r : 0] : 0.0);
+            pl[s] = pl[s] + (r < M ? nn_log(a[LF::at(r < M ? r : 0, r < M ? r : 0)]) : 0.0);
+        }
+    }
+#pragma unroll
+    for (int st = 1; st < 16; st <<= 1)
+#pragma unroll
+        for (int s = 0; s < 16; s += 2 * st) {
+            py[s] = py[s] + py[s + st];
+            pl[s] = pl[s] + pl[s + st];
+        }
+    const double res = -(((-0.5 * py[0]) - pl[0]) - ((double)M / 2) * LOG_2PI);
+    return (bad || res != res) ? INFINITY : res;
+}
+
+// One fit per lane; unfused batched mode (blockIdx.y = prediction), work queue per prediction.
+template <int M>
+__global__ void __launch_bounds__(256) nm_lane1_kernel(NMArgs a) {
+    if (a.skip && *a.skip) return;
+    nm_batch_offsets(a);
+    const int nfc = a.nj * a.R;
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double *sD2 = sm;
+    const int tid = threadIdx.x;
+    double *ys = sm + M * M + tid;   // this lane's y column, row r at ys[r * 256]
+    for (int i = tid; i < M * M; i += blockDim.x) sD2[i] = a.D2[i];
+    __syncthreads();
+    NMCfg cfg{a.fatol, a.xatol, a.maxfev, a.maxfev};
+    NM St;
+    double jit = 1.0;
+    int fn = blockIdx.x * blockDim.x + tid, f = 0;
+    bool valid = false;
+    auto start_fit = [&]() {
+        valid = fn < a.n_fits;
+        f = fn;
+        if (valid && a.jmajor && !a.coord) f = (fn % a.d) * nfc + fn / a.d;
+        int coord = 0, jidx = 0;
+        if (valid) {
+            if (a.coord) {
+                coord = a.coord[f];
+                jidx = a.jitter_idx[f];
+            } else {   // product(coord, jitter, restart) order (models.py:186)
+                coord = f / nfc;
+                jidx = (f % nfc) / a.R;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < M; r++) ys[r * 256] = valid ? a.Y[(int64_t)coord * a.ys_c + (int64_t)r * a.ys_r] : 0.0;
+        jit = valid ? jit_lookup(a, jidx) : 1.0;
+        St.f0 = St.f1 = St.f2 = INFINITY;
+        St.xbx = St.xby = St.xrx = St.xry = St.fxr = 0.0;
+        if (valid) {
+            nm_start(St, cfg, a.theta0[2 * f], a.theta0[2 * f + 1]);
+        } else {
+            St.s0x = St.s0y = St.s1x = St.s1y = St.s2x = St.s2y = 0.0;
+            St.px = St.py = 0.0;
+            St.fcalls = St.iters = 0;
+            St.st = ST_DONE;
+        }
+    };
+    auto write_fit = [&]() {
+        if (!valid) return;
+        const double fval = (St.f1 != St.f1 || St.f2 != St.f2) ? NAN : St.f0;
+        if (a.theta_out) { a.theta_out[2 * f] = St.s0x; a.theta_out[2 * f + 1] = St.s0y; }
+        if (a.fval_out) a.fval_out[f] = fval;
+        if (a.nfev_out) a.nfev_out[f] = St.fcalls;
+        if (a.fits_out) {
+            a.fits_out[4 * f + 0] = St.s0x;
+            a.fits_out[4 * f + 1] = St.s0y;
+            a.fits_out[4 * f + 2] = fval;
+            a.fits_out[4 * f + 3] = (double)St.fcalls;
+        }
+        if (a.done) {   // the fit is visible device-wide before it is counted
+            __threadfence();
+            __hip_atomic_fetch_add(a.done + blockIdx.y, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+    start_fit();
+    bool can_take = a.queue != nullptr && valid;
+    // every lane evaluates once per trip until the wave's last fit is done (finished lanes
+    // evaluate their last point again, discarded); a finished lane first takes the next
+    // unassigned fit of its prediction from the queue
+    while (true) {
+        if (can_take && St.st == ST_DONE) {
+            write_fit();
+            fn = (int)(gridDim.x * blockDim.x) + atomicAdd(a.queue + blockIdx.y, 1);
+            start_fit();
+            can_take = valid;
+        }
+        const bool need = St.st != ST_DONE;
+        if (!__any(need)) break;
+        const double fv = lane1_nlml<M>(sD2, St.px, St.py, jit, ys);
+        if (need) nm_consume(St, cfg, fv);
+    }
+    write_fit();
+}
+
+// instantiated neighbour counts: the speculative batches of the BASELINE configs (Burgers nn = 15,
+// Hopf / Lorenz 10-15).  LPF = 4 (lane_nlml) or 1 (lane1_nlml, NNGP_NM_LPF=1).  (m >= 17 needs
+// more than a lane's 256 VGPRs at LPF = 4 -- the packed kernel serves it.)
 template <typename F>
 static int with_lane_m(int m, F &&f) {
     switch (m) {
@@ -371,25 +631,59 @@ bool nm_lanes_supported(int m) {
     return with_lane_m(m, [](auto) { return NNGP_OK; }) == NNGP_OK;
 }
 
+static int lanes_lpf() {
+    return env_int("NNGP_NM_LPF", 4) == 1 ? 1 : 4;
+}
+
+// Grid of a batched launch: the work queue lets a group (LPF lanes) that finished its fit take the
+// next unassigned fit of its prediction, so the grid only has to fill the chip once -- #CU x 4
+// SIMDs x the kernel's waves per SIMD (its registers: 2 at LPF = 4, 1 at LPF = 1), spread over the
+// nq predictions -- and never needs more workgroups than a prediction has fits (one fit per
+// group, no queue).  (A fixed "8 fits per group" grid, round 5's first cut, left a one-prediction
+// batch of 18 432 fits on 144 waves: 5.4 ms against 1.65 ms on the packed kernel,
+// profiles/r05/nm_lanes/.)  NNGP_NM_REFILL = 0 / 1: no queue, one fit per group.
+static int lanes_grid(NMArgs &a, hipStream_t st, int nq, int qslot, int threads, int ngroups, int waves_per_simd,
+                      int &nblocks) {
+    const int full = (a.n_fits + ngroups - 1) / ngroups;   // one fit per group
+    nblocks = full;
+    a.queue = nullptr;
+    if (env_int("NNGP_NM_REFILL", 8) <= 1 || full <= 1) return NNGP_OK;
+    const int64_t resident = (int64_t)device_cus() * 4 * waves_per_simd / (threads / 64);   // workgroups
+    const int per_pred = (int)std::max<int64_t>(1, (resident + nq - 1) / nq);
+    if (per_pred >= full) return NNGP_OK;
+    int err = 0;
+    int32_t *qbuf = (int32_t *)workspace(sizeof(int32_t) * (size_t)nq, &err, qslot);
+    if (err) return err;
+    NNGP_HIP_CHECK(hipMemsetAsync(qbuf, 0, sizeof(int32_t) * (size_t)nq, st));
+    a.queue = qbuf;
+    nblocks = per_pred;
+    return NNGP_OK;
+}
+
 int run_nm_lanes(NMArgs &a, hipStream_t st, int nq, int qslot) {
+    if (lanes_lpf() == 1) {
+        return with_lane_m(a.m, [&](auto mc) {
+            constexpr int M = decltype(mc)::value;
+            const int threads = 256;
+            int nblocks = 0;
+            const int err = lanes_grid(a, st, nq, qslot, threads, threads, 1, nblocks);
+            if (err) return err;
+            hipLaunchKernelGGL((nm_lane1_kernel<M>), dim3(nblocks, nq), dim3(threads),
+                               sizeof(double) * (M * M + 256 * M), st, a);
+            NNGP_LAUNCH_CHECK();
+            return NNGP_OK;
+        });
+    }
     return with_lane_m(a.m, [&](auto mc) {
-        constexpr int M = decltype(mc)::value, LPF = LaneLPF<M>::V;
-        // workgroup size (NNGP_NM_LANES_WG: 64 / 128 / 256): the kernel runs one wave per SIMD
-        // (its VGPRs), so smaller workgroups free a SIMD as soon as their wave's fits are done
+        constexpr int M = decltype(mc)::value, LPF = 4;
+        // workgroup size (NNGP_NM_LANES_WG: 64 / 128 / 256): smaller workgroups free a SIMD as soon
+        // as their wave's fits are done
         const int wg = env_int("NNGP_NM_LANES_WG", 256);
         const int threads = (wg == 64 || wg == 128) ? wg : 256, ngroups = threads / LPF;
         const size_t lds = sizeof(double) * ((size_t)M * M + (size_t)ngroups * LaneFit<M, LPF>::IMG);
-        int nblocks = (a.n_fits + ngroups - 1) / ngroups;
-        a.queue = nullptr;
-        const int per_group = std::max(0, env_int("NNGP_NM_REFILL", 8));
-        if (per_group > 1 && nblocks > 1) {   // work queues: ~per_group fits per group on average
-            int err = 0;
-            int32_t *qbuf = (int32_t *)workspace(sizeof(int32_t) * (size_t)nq, &err, qslot);
-            if (err) return err;
-            NNGP_HIP_CHECK(hipMemsetAsync(qbuf, 0, sizeof(int32_t) * (size_t)nq, st));
-            a.queue = qbuf;
-            nblocks = std::max(1, (nblocks + per_group - 1) / per_group);
-        }
+        int nblocks = 0;
+        const int err = lanes_grid(a, st, nq, qslot, threads, ngroups, 2, nblocks);
+        if (err) return err;
         hipLaunchKernelGGL((nm_lane_kernel<M, LPF>), dim3(nblocks, nq), dim3(threads), lds, st, a);
         NNGP_LAUNCH_CHECK();
         return NNGP_OK;

@@ -260,14 +260,16 @@ def test_nm_fit_batch_vs_oracle(gpu, m, d, tol):
     assert exact == len(coords)   # shared exp/log/10^x: bitwise
 
 
+@pytest.mark.parametrize('lpf', ['4', '1'])
 @pytest.mark.parametrize('m,d,dup', [(10, 3, False), (15, 3, True), (15, 128, False), (15, 128, True)])
-def test_nm_lanes_kernel_vs_oracle(gpu, m, d, dup, monkeypatch):
+def test_nm_lanes_kernel_vs_oracle(gpu, m, d, dup, lpf, monkeypatch):
     """The throughput fits kernel (csrc/nngp_nmlane.hip: 4 lanes per fit, exact m, work queue;
     forced by NNGP_NM_LANES=1) through nngp_nm_fit_batch: every fit -- theta, -LML and nfev -- bit
     for bit the oracle's Nelder-Mead (oracle/nngp_oracle.c orc_nm_fit).  d = 128: all 1 152
     (coordinate, jitter) fits of a Burgers-sized prediction; dup: two neighbours coincide, so the
     low-jitter kernels are singular and their Cholesky fails (NaN -> +inf) on the way."""
     monkeypatch.setenv('NNGP_NM_LANES', '1')
+    monkeypatch.setenv('NNGP_NM_LPF', lpf)   # 4 lanes per fit, or one fit per lane
     mdl = gpu.NNGP_p(n=d, N=4, fatol=0.1, xatol=0.1, seed=7)
     xm, ym = _nm_case(m, d, m * 100 + d + 1)
     if dup:
