@@ -1787,7 +1787,10 @@ static int run_mean(NMArgs &a, hipStream_t st) {
 // speculative kernel: one wave per fit, 4 fits per 256-thread workgroup (1 per 64-thread
 // workgroup for m > 32)
 // waves per fit of the two-level kernel for a launch of `total` fits: 4 while every fit's four
-// waves get a SIMD of their own (total <= #CU), 2 up to twice that, else the one-level kernel.
+// waves get a SIMD of their own (total <= #CU), 2 up to twice that -- and, for two row sets per
+// lane (MAXM 18..32, whose one-level evaluation is twice as long), up to four times that: the
+// FHN-PDE d = 800 8-GPU share (100 coordinates, 900 fits at m = 20) 0.711 -> 0.644 ms per
+// correction, 4 waves 0.836 (profiles/r05/fhn_corr/level2.txt) -- else the one-level kernel.
 // (Resumed parked fits take their shape on the device instead: run_nm_spec / resume_bounds.)
 // NNGP_NM_LEVEL2=0 disables it.
 static int spec_waves(int total, int maxm, bool resume) {
@@ -1795,7 +1798,7 @@ static int spec_waves(int total, int maxm, bool resume) {
     if (maxm > 32 || resume || e == 0) return 1;
     if (e == 2 || e == 4) return e;   // forced (measurements)
     const int ncu = device_cus();
-    return total <= ncu ? 4 : (total <= 2 * ncu ? 2 : 1);
+    return total <= ncu ? 4 : (total <= (maxm > 16 ? 4 : 2) * ncu ? 2 : 1);
 }
 
 // Finite parked-fit counts up to which the resume gives each finite fit 4 / 2 waves of the

@@ -636,19 +636,25 @@ static int lanes_lpf() {
 }
 
 // Grid of a batched launch: the work queue lets a group (LPF lanes) that finished its fit take the
-// next unassigned fit of its prediction, so the grid only has to fill the chip once -- #CU x 4
-// SIMDs x the kernel's waves per SIMD (its registers: 2 at LPF = 4, 1 at LPF = 1), spread over the
-// nq predictions -- and never needs more workgroups than a prediction has fits (one fit per
-// group, no queue).  (A fixed "8 fits per group" grid, round 5's first cut, left a one-prediction
-// batch of 18 432 fits on 144 waves: 5.4 ms against 1.65 ms on the packed kernel,
-// profiles/r05/nm_lanes/.)  NNGP_NM_REFILL = 0 / 1: no queue, one fit per group.
-static int lanes_grid(NMArgs &a, hipStream_t st, int nq, int qslot, int threads, int ngroups, int waves_per_simd,
+// next unassigned fit of its prediction, so the grid only has to fill the chip once -- the
+// workgroups the occupancy calculator says fit at a time (registers and LDS: at 256 threads the
+// 4-lane kernel's LDS images allow one workgroup per CU), spread over the nq predictions -- and
+// never needs more workgroups than a prediction has fits (one fit per group, no queue).  A
+// fixed "8 fits per group" grid, round 5's first cut, left a one-prediction batch of 18 432 fits
+// on 144 waves (profiles/r05/nm_lanes/).  NNGP_NM_LANES_FILL (percent, default 100) sizes the
+// grid to that share of the resident workgroups: the batch shares the chip with the sweep it
+// feeds.  NNGP_NM_REFILL = 0 / 1: no queue, one fit per group.
+template <typename K>
+static int lanes_grid(NMArgs &a, hipStream_t st, int nq, int qslot, K kernel, int threads, size_t lds, int ngroups,
                       int &nblocks) {
     const int full = (a.n_fits + ngroups - 1) / ngroups;   // one fit per group
     nblocks = full;
     a.queue = nullptr;
     if (env_int("NNGP_NM_REFILL", 8) <= 1 || full <= 1) return NNGP_OK;
-    const int64_t resident = (int64_t)device_cus() * 4 * waves_per_simd / (threads / 64);   // workgroups
+    int per_cu = 0;
+    NNGP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds));
+    const int fill = std::min(100, std::max(1, env_int("NNGP_NM_LANES_FILL", 100)));
+    const int64_t resident = std::max<int64_t>(1, (int64_t)std::max(per_cu, 1) * device_cus() * fill / 100);
     const int per_pred = (int)std::max<int64_t>(1, (resident + nq - 1) / nq);
     if (per_pred >= full) return NNGP_OK;
     int err = 0;
@@ -665,11 +671,11 @@ int run_nm_lanes(NMArgs &a, hipStream_t st, int nq, int qslot) {
         return with_lane_m(a.m, [&](auto mc) {
             constexpr int M = decltype(mc)::value;
             const int threads = 256;
+            const size_t lds = sizeof(double) * (M * M + 256 * M);
             int nblocks = 0;
-            const int err = lanes_grid(a, st, nq, qslot, threads, threads, 1, nblocks);
+            const int err = lanes_grid(a, st, nq, qslot, nm_lane1_kernel<M>, threads, lds, threads, nblocks);
             if (err) return err;
-            hipLaunchKernelGGL((nm_lane1_kernel<M>), dim3(nblocks, nq), dim3(threads),
-                               sizeof(double) * (M * M + 256 * M), st, a);
+            hipLaunchKernelGGL((nm_lane1_kernel<M>), dim3(nblocks, nq), dim3(threads), lds, st, a);
             NNGP_LAUNCH_CHECK();
             return NNGP_OK;
         });
@@ -682,7 +688,7 @@ int run_nm_lanes(NMArgs &a, hipStream_t st, int nq, int qslot) {
         const int threads = (wg == 64 || wg == 128) ? wg : 256, ngroups = threads / LPF;
         const size_t lds = sizeof(double) * ((size_t)M * M + (size_t)ngroups * LaneFit<M, LPF>::IMG);
         int nblocks = 0;
-        const int err = lanes_grid(a, st, nq, qslot, threads, ngroups, 2, nblocks);
+        const int err = lanes_grid(a, st, nq, qslot, nm_lane_kernel<M, LPF>, threads, lds, ngroups, nblocks);
         if (err) return err;
         hipLaunchKernelGGL((nm_lane_kernel<M, LPF>), dim3(nblocks, nq), dim3(threads), lds, st, a);
         NNGP_LAUNCH_CHECK();
