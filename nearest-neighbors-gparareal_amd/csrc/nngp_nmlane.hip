@@ -655,7 +655,10 @@ static int lanes_grid(NMArgs &a, hipStream_t st, int nq, int qslot, K kernel, in
     NNGP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds));
     const int fill = std::min(100, std::max(1, env_int("NNGP_NM_LANES_FILL", 100)));
     const int64_t resident = std::max<int64_t>(1, (int64_t)std::max(per_cu, 1) * device_cus() * fill / 100);
-    const int per_pred = (int)std::max<int64_t>(1, (resident + nq - 1) / nq);
+    // (rounded down: a rounded-up share left the last predictions' workgroups waiting for a slot
+    // and running after everything else -- Burgers' 125-prediction batch, 3 x 125 workgroups for
+    // 256 slots, took 9 ms in the run against 6.4 ms for one prediction of the same fit count)
+    const int per_pred = (int)std::max<int64_t>(1, resident / nq);
     if (per_pred >= full) return NNGP_OK;
     int err = 0;
     int32_t *qbuf = (int32_t *)workspace(sizeof(int32_t) * (size_t)nq, &err, qslot);
@@ -682,9 +685,10 @@ int run_nm_lanes(NMArgs &a, hipStream_t st, int nq, int qslot) {
     }
     return with_lane_m(a.m, [&](auto mc) {
         constexpr int M = decltype(mc)::value, LPF = 4;
-        // workgroup size (NNGP_NM_LANES_WG: 64 / 128 / 256): smaller workgroups free a SIMD as soon
-        // as their wave's fits are done
-        const int wg = env_int("NNGP_NM_LANES_WG", 256);
+        // workgroup size (NNGP_NM_LANES_WG: 64 / 128 / 256): the LDS images allow 1 / 3 / 7
+        // workgroups of 256 / 128 / 64 threads per CU.  Burgers N = 128 to convergence (medians of
+        // 3, profiles/r05/nm_lanes/grid_floor_ab_wg.txt): 0.231 / 0.221 / 0.223 s
+        const int wg = env_int("NNGP_NM_LANES_WG", 128);
         const int threads = (wg == 64 || wg == 128) ? wg : 256, ngroups = threads / LPF;
         const size_t lds = sizeof(double) * ((size_t)M * M + (size_t)ngroups * LaneFit<M, LPF>::IMG);
         int nblocks = 0;
