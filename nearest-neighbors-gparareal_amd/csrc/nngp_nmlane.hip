@@ -1,5 +1,6 @@
-// nngp_nmlane.hip -- the throughput-shaped Nelder-Mead fits kernel: LPF (2 or 4) lanes per fit,
-// the exact neighbour count M as a compile-time constant (no padding).
+// nngp_nmlane.hip -- the throughput-shaped Nelder-Mead fits kernels: LPF = 4 lanes per fit
+// (nm_lane_kernel, the default) or one (nm_lane1_kernel, NNGP_NM_LPF=1), the exact neighbour count
+// M as a compile-time constant (no padding).
 //
 // Reference: NNGP_p.get_preds fans d*9*R independent fits out through pool.map (models.py:185-202);
 // each is scipy's Nelder-Mead (models.py:254-260) on the -LML of _fit_gp_jit (models.py:86-92,
@@ -424,7 +425,10 @@ template <int M> struct Lane1 {
     static constexpr int tail_start(int j) { return j + 1 + ((M - 1 - j) & ~3); }
 };
 
-// ys: this lane's y column in LDS, row r at ys[r * 256]
+// threads of the one-fit-per-lane kernel's workgroup = the row stride of its LDS y columns
+static constexpr int LANE1_THREADS = 256;
+
+// ys: this lane's y column in LDS, row r at ys[r * LANE1_THREADS]
 template <int M>
 __device__ __forceinline__ double lane1_nlml(const double *D2, double sx, double sy, double jit, const double *ys) {
     using LF = Lane1<M>;
@@ -496,7 +500,7 @@ __device__ __forceinline__ double lane1_nlml(const double *D2, double sx, double
     double z[M];
     static_for<0, M>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        double acc = ys[i * 256];
+        double acc = ys[i * LANE1_THREADS];
 #pragma unroll
         for (int k = 0; k < i; k++) acc = acc - a[LF::at(i, k)] * z[k];
         z[i] = mk_div(acc, a[LF::at(i, i)], ri[i]);
@@ -513,12 +517,12 @@ __device__ __forceinline__ double lane1_nlml(const double *D2, double sx, double
     double py[16], pl[16];
 #pragma unroll
     for (int s = 0; s < 16; s++) {
-        py[s] = s < M ? ys[(s < M ? s : 0) * 256] * z[s < M ? s : 0] : 0.0;
+        py[s] = s < M ? ys[(s < M ? s : 0) * LANE1_THREADS] * z[s < M ? s : 0] : 0.0;
         pl[s] = s < M ? nn_log(a[LF::at(s < M ? s : 0, s < M ? s : 0)]) : 0.0;
 #pragma unroll
         for (int f = 1; 16 * f < M; f++) {
             const int r = s + 16 * f;
-            py[s] = py[s] + (r < M ? ys[(r < M ? r : 0) * 256] * z[r < M ? r : 0] : 0.0);
+            py[s] = py[s] + (r < M ? ys[(r < M ? r : 0) * LANE1_THREADS] * z[r < M ? r : 0] : 0.0);
             pl[s] = pl[s] + (r < M ? nn_log(a[LF::at(r < M ? r : 0, r < M ? r : 0)]) : 0.0);
         }
     }
@@ -535,14 +539,14 @@ __device__ __forceinline__ double lane1_nlml(const double *D2, double sx, double
 
 // One fit per lane; unfused batched mode (blockIdx.y = prediction), work queue per prediction.
 template <int M>
-__global__ void __launch_bounds__(256) nm_lane1_kernel(NMArgs a) {
+__global__ void __launch_bounds__(LANE1_THREADS) nm_lane1_kernel(NMArgs a) {
     if (a.skip && *a.skip) return;
     nm_batch_offsets(a);
     const int nfc = a.nj * a.R;
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double *sD2 = sm;
     const int tid = threadIdx.x;
-    double *ys = sm + M * M + tid;   // this lane's y column, row r at ys[r * 256]
+    double *ys = sm + M * M + tid;   // this lane's y column, row r at ys[r * LANE1_THREADS]
     for (int i = tid; i < M * M; i += blockDim.x) sD2[i] = a.D2[i];
     __syncthreads();
     NMCfg cfg{a.fatol, a.xatol, a.maxfev, a.maxfev};
@@ -565,7 +569,7 @@ __global__ void __launch_bounds__(256) nm_lane1_kernel(NMArgs a) {
             }
         }
 #pragma unroll
-        for (int r = 0; r < M; r++) ys[r * 256] = valid ? a.Y[(int64_t)coord * a.ys_c + (int64_t)r * a.ys_r] : 0.0;
+        for (int r = 0; r < M; r++) ys[r * LANE1_THREADS] = valid ? a.Y[(int64_t)coord * a.ys_c + (int64_t)r * a.ys_r] : 0.0;
         jit = valid ? jit_lookup(a, jidx) : 1.0;
         St.f0 = St.f1 = St.f2 = INFINITY;
         St.xbx = St.xby = St.xrx = St.xry = St.fxr = 0.0;
@@ -673,8 +677,8 @@ int run_nm_lanes(NMArgs &a, hipStream_t st, int nq, int qslot) {
     if (lanes_lpf() == 1) {
         return with_lane_m(a.m, [&](auto mc) {
             constexpr int M = decltype(mc)::value;
-            const int threads = 256;
-            const size_t lds = sizeof(double) * (M * M + 256 * M);
+            const int threads = LANE1_THREADS;
+            const size_t lds = sizeof(double) * (M * M + LANE1_THREADS * M);
             int nblocks = 0;
             const int err = lanes_grid(a, st, nq, qslot, nm_lane1_kernel<M>, threads, lds, threads, nblocks);
             if (err) return err;

@@ -89,9 +89,9 @@ def test_published_burgers59_nngp_straddle_over_seeds(gpu):
 # --------------------------------------------------------------------------------- long (opt-in)
 @LONG
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize('name', ['hopf_512_para', 'hopf_128_para'])
+@pytest.mark.parametrize('name', ['hopf_512_para', 'hopf_128_para', 'hopf_32_para'])
 def test_published_hopf_parareal_k_exact(gpu, name):
-    """Hopf.py Parareal N = 512 (K = 149, 276 s) and N = 128 (K = 54, 430 s)."""
+    """Hopf.py Parareal N = 512 (K = 149, 276 s), N = 128 (K = 54, 430 s), N = 32 (K = 19, 590 s)."""
     out, pk = _run(gpu, name)
     assert out['converged'] and out['K'] == pk
 
