@@ -2208,10 +2208,9 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
     a.jmajor = env_int("NNGP_NM_JMAJOR", 1);   // (run_nm_parked; Burgers 0.328 -> 0.317 s)
     a.done = done;
     // latency: a wave per fit (the re-speculation window the sweep waits on); else packed fits.
-    // NNGP_RESPEC_SHAPE (measurements): 1 runs the window's fits packed, 2 on the 4-lanes kernel
-    const int shape = latency ? env_int("NNGP_RESPEC_SHAPE", 0) : 0;
-    if (latency && shape == 0) return run_nm_spec(a, st, nq);
-    if (shape == 2 && nm_lanes_supported(m)) return run_nm_lanes(a, st, nq, 8);
+    // (The window on the packed or the 4-lanes kernel: Burgers 0.297 / 0.281 s against 0.221 s,
+    // profiles/r05/nm_lanes/respec_shape_not_kept.txt -- the next slice waits on its slowest fit.)
+    if (latency) return run_nm_spec(a, st, nq);
     return run_nm(a, false, st, nq, slot == 1 ? 7 : 8);
 }
 

@@ -42,7 +42,7 @@ KNOBS = [
     ('fhn512', 'NNGP_RESUME_W2', '0'), ('burgers', 'NNGP_SPEC_WAIT_US', '0'), ('burgers', 'NNGP_GUESS_FUSED', '0'),
     ('lorenz', 'NNGP_GUESS_FUSED', '0'), ('lorenz', 'NNGP_CHAIN_BARRIER_US', '0'),
     ('burgers', 'NNGP_NM_LANES', '0'), ('burgers', 'NNGP_NM_LANES', '1'), ('lorenz', 'NNGP_NM_LANES', '1'),
-    ('burgers', 'NNGP_NM_LANES_WG', '64'), ('burgers', 'NNGP_NM_LPF', '1'), ('burgers', 'NNGP_NM_LPF', '4'), ('burgers', 'NNGP_NM_LANES_FILL', '50'), ('burgers', 'NNGP_RESPEC_SHAPE', '2'),
+    ('burgers', 'NNGP_NM_LANES_WG', '64'), ('burgers', 'NNGP_NM_LPF', '1'), ('burgers', 'NNGP_NM_LPF', '4'), ('burgers', 'NNGP_NM_LANES_FILL', '50'),
 ]
 # knobs whose neutrality needs a setting these runs do not have, tested where they apply:
 # NNGP_SHARD_EMULATE_RANKS (a one-rank RCCL communicator: test_gpu_distributed.py
