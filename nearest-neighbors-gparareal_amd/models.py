@@ -389,6 +389,9 @@ class GPjax_p(ModelAbstr):
         self.train_count = np.zeros(N)
         self.k = 0
         self.rounds = []
+        # per training call: training rows and the likelihood evaluations its fits made (sum of
+        # nfev = the (rows+1)^2 matrices factored), for the measured Cholesky rate (bench.py)
+        self.call_rows, self.call_evals = [], []
         self._dev = None   # (X [rows][n], alpha [n][rows], coef [n][2]) device tensors
         # multi-GPU (the reference's pool.map over the d*9 fits, models.py:386-392):
         # the torch.distributed group the fits are sharded over by coordinate (Parareal sets it;
@@ -424,6 +427,8 @@ class GPjax_p(ModelAbstr):
         self.tot_train_t[min(self.k, self.N - 1)] += time.time() - st
         self.train_count[min(self.k, self.N - 1)] += nf
         self.rounds.append(int(rounds.value))
+        self.call_rows.append(int(X.shape[0]))
+        self.call_evals.append(int(ne.astype(np.int64).sum()))
         return th, fv, ne
 
     def _train_coord_rnd(self, X, Y, coord):
