@@ -66,22 +66,48 @@ constexpr int N_WS_SLOTS = 10;   // slot 2: the sweep's speculation buffers; 3: 
                                 // 9: the sharded sweep's zeros (nngp_comm.hip)
 void *workspace(size_t bytes, int *err, int slot = 0);
 
+// A prepared coordinate of gp_pre_kernel: alpha rows 0..maxm-1 | c | psy | ok
+__host__ __device__ constexpr int HM_STRIDE(int maxm) { return maxm + 3; }
+
+// The sweep's split prediction (nngp_sweep.hip): a select whose ordered list hits a speculative
+// prediction that gp_pre_kernel has already prepared (done[0] == target) finishes the slice's
+// posterior mean itself -- from the prepared coordinates and the query's kd2, gp_mean_finish --
+// and reports hit + 2 to the host, which then launches no mean kernel for the slice.
+struct HitMean {
+    const double *AP1, *AP2;          // the slice's prepared coordinates for hit 1 / hit 2 (or null)
+    const int32_t *done1, *done2;     // their gp_pre workgroup counters (the slice's entry)
+    int target;                       // gp_pre workgroups per prediction
+    int maxm;                         // the padded fit size the coordinates were prepared at
+    const double *bias;               // UG1[i+1]
+    double *out, *preds;              // U1[i+1] = mean + bias, preds = mean
+};
+
 // predict_impl's launches in parts (the speculative sweep issues the select, reads its hit flag on
 // the host, and then launches the fits only on a miss): all | kNN + select | fits + mean | mean only
-enum { PREDICT_ALL = 0, PREDICT_SELECT = 1, PREDICT_FITS_MEAN = 2, PREDICT_MEAN = 3 };
+enum { PREDICT_ALL = 0, PREDICT_SELECT = 1, PREDICT_FITS_MEAN = 2, PREDICT_MEAN = 3, PREDICT_SELECT_ONLY = 4 };
+// the slice head G(U1[i]) + the query's distances as one launch (gdist_kernel): PREDICT_SELECT_ONLY
+// then launches the select alone.  gdist_supported: systems with an in-kernel G (NNGP_GDIST=0: off)
+bool gdist_supported(const nngp_system *sys, int g_step_mode);
+int gdist(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps, const double *t, int i,
+          const double *X, int64_t rows, int d, int m, int n_jitter, int n_restarts, const double *ui,
+          double *ug_next, hipStream_t st);
 int predict_impl(const double *X, const double *Y, int64_t rows, int d, const double *new_x, int m,
                  int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
                  double fatol, double xatol, int maxfev, double *preds_out, const double *bias,
                  double *out, double *fits_out, const int32_t *spec_idx, const double *spec_fits,
                  int32_t *hit_flag, const int32_t *spec2_idx, const double *spec2_fits, int32_t *host_flag,
                  hipStream_t st, int c0 = 0, int c1 = -1, const int32_t *wait_done = nullptr,
-                 int32_t *wait_err = nullptr, int phase = PREDICT_ALL);
+                 int32_t *wait_err = nullptr, int phase = PREDICT_ALL, const HitMean *hm = nullptr);
 int gpfull_mean(const double *X, int64_t rows, int d, const double *q, const double *coef, const double *alpha,
                 const double *bias, double *out, hipStream_t st);
 int spec_batch(const double *X, const double *Y, int64_t rows, int d, const double *Q, int nq, int m,
                int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
                double fatol, double xatol, int maxfev, int32_t *idx_out, double *fits_out, bool latency,
-               hipStream_t st, int slot = 1, int32_t *done = nullptr, hipEvent_t ev_select = nullptr);
+               hipStream_t st, int slot = 1, int32_t *done = nullptr, hipEvent_t ev_select = nullptr,
+               double *pre_AP = nullptr, int32_t *pre_done = nullptr);
+// gp_pre_kernel's workgroups per prediction (the HitMean target) for d coordinates at fit size m
+int pre_target(int d, int m);
+int pre_maxm(int m);   // the padded fit size of m
 // the fused correction chain (nngp_gp.hip): one persistent kernel per run of hit slices
 void chain_release();   // nngp_shutdown's parts (nngp_gp.hip / nngp_sweep.hip / nngp_comm.hip)
 void sweep_release();

@@ -297,7 +297,7 @@ struct SelShm {
 template <int K> __global__ void knn_select_kernel(const double *, int64_t, int, const double *, const double *, int,
                                                   const double *, int32_t *, double *, double *, double *,
                                                   double *, const int32_t *, int32_t *, int, const int32_t *,
-                                                  int32_t *);
+                                                  int32_t *, HitMean);
 
 // register-resident keys when rows <= 256*K (K = 2..16), else the streaming form (K = 0)
 template <typename... A>
@@ -360,7 +360,8 @@ __device__ __forceinline__ void knn_select_dev(
     const double *__restrict__ Y, int d, const double *__restrict__ q, int32_t *__restrict__ idx_out,
     double *__restrict__ dist_out, double *__restrict__ ymT, double *__restrict__ D2,
     double *__restrict__ kd2, const int32_t *__restrict__ spec_idx, int32_t *__restrict__ hit_flag,
-    int xs_doubles, const int32_t *__restrict__ spec2_idx, int32_t *host_flag, uint64_t *marks = nullptr) {
+    int xs_doubles, const int32_t *__restrict__ spec2_idx, int32_t *host_flag, uint64_t *marks = nullptr,
+    const HitMean *hm = nullptr) {
     // marks (profiling, thread 0's clock): after the rounds | the merges | the gathers | D2
 #define SEL_MARK(k) \
     if (marks && tid == 0) marks[k] += wall_clock64();
@@ -548,6 +549,9 @@ __device__ __forceinline__ void knn_select_dev(
         if (dist_out) dist_out[k] = seld[k];
     }
     SEL_MARK(1);
+    // the hit code; with hm, whether this select also finishes the mean (the prediction it hit is
+    // prepared).  Without it the host flag is written here; with it, after the mean.
+    __shared__ int s_hm;
     if (hit_flag && wid == 0) {   // lane k compares entry k of the lists: one round trip, not m
         bool ne1 = false, ne2 = spec2_idx == nullptr;
         for (int k = lane; k < m; k += 64) {
@@ -559,14 +563,28 @@ __device__ __forceinline__ void knn_select_dev(
         const int hit = hit1 ? 1 : (hit2 ? 2 : 0);
         if (lane == 0) {
             *hit_flag = hit;
-            if (host_flag) __hip_atomic_store(host_flag, hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            int hmv = 0;
+            if (hm && hit != 0) {
+                const double *ap = hit == 1 ? hm->AP1 : hm->AP2;
+                const int32_t *dn = hit == 1 ? hm->done1 : hm->done2;
+                if (ap && __hip_atomic_load(dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= hm->target) {
+                    __threadfence();   // the prepared coordinates before their count
+                    hmv = hit;
+                }
+            }
+            s_hm = hmv;
+            if (host_flag && hmv == 0) __hip_atomic_store(host_flag, hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+    } else if (tid == 0) {
+        s_hm = 0;
     }
+    __syncthreads();
+    const int hm_hit = s_hm;   // uniform: 1 / 2 = finish the mean from AP1 / AP2 below
     // the gathers of the m selected rows: SG loads in flight per thread before their stores (a
     // load -> store per trip would wait out one memory latency per element)
     constexpr int SG = 8;
     const int md = m * d;
-    if (ymT) {   // coalesced row reads, transposed writes
+    if (ymT && hm_hit == 0) {   // coalesced row reads, transposed writes (a finished hit reads none)
         for (int t0 = tid; t0 < md; t0 += 256 * SG) {
             double v[SG];
 #pragma unroll
@@ -609,9 +627,11 @@ __device__ __forceinline__ void knn_select_dev(
         const int ntask = npairs + (kd2 ? m : 0);
         if (staged && d >= 8 && d <= 128) {   // an octet of lanes per pair (pw_leaf_octet)
             const int j8 = tid & 7;
-            const int nrnd = (ntask + 31) / 32;   // whole octets iterate together
+            // a finished hit needs kd2 only (its D2 is the prepared prediction's): tasks npairs..
+            const int t0 = hm_hit != 0 ? npairs : 0;
+            const int nrnd = (ntask - t0 + 31) / 32;   // whole octets iterate together
             for (int rd = 0; rd < nrnd; rd++) {
-                const int t = rd * 32 + (tid >> 3);
+                const int t = t0 + rd * 32 + (tid >> 3);
                 const bool valid = t < ntask;
                 const bool is_kd = valid && t >= npairs;
                 int r = 0, jj = 0;
@@ -678,6 +698,47 @@ __device__ __forceinline__ void knn_select_dev(
     __syncthreads();
     SEL_MARK(3);
 #undef SEL_MARK
+    if (hm_hit != 0) {   // gp_mean_dev's output for every coordinate, from the prepared halves
+        const double *AP = hm_hit == 1 ? hm->AP1 : hm->AP2;
+        const int l = tid & 15, grp = tid >> 4, maxm = hm->maxm, rpl = (maxm + 15) / 16, st = HM_STRIDE(maxm);
+        const bool big = maxm > 32;
+        double kd[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) kd[s] = kd2[l + 16 * s < m ? l + 16 * s : 0];
+        // CH coordinates per group at a time, all their loads issued before the sums; every group
+        // runs every trip (the DPP row sums)
+        constexpr int CH = 4;
+        for (int c0 = 0; c0 < d; c0 += 16 * CH) {
+            double al[CH][4], cq[CH], ps[CH], okv[CH];
+#pragma unroll
+            for (int u = 0; u < CH; u++) {
+                const int c = c0 + 16 * u + grp;
+                const double *ap = AP + (int64_t)(c < d ? c : 0) * st;
+#pragma unroll
+                for (int s = 0; s < 4; s++) {
+                    const int row = l + 16 * s;
+                    al[u][s] = (s < rpl && row < maxm) ? ap[row] : 0.0;
+                }
+                cq[u] = ap[maxm];
+                ps[u] = ap[maxm + 1];
+                okv[u] = ap[maxm + 2];
+            }
+#pragma unroll
+            for (int u = 0; u < CH; u++) {
+                const int c = c0 + 16 * u + grp;
+                const double mean = gp_mean_finish<4>(m, l, rpl, big, kd, cq[u], ps[u], al[u], okv[u] != 0.0);
+                if (c < d && l == 0) {
+                    hm->preds[c] = mean;
+                    hm->out[c] = mean + hm->bias[c];
+                }
+            }
+        }
+        __syncthreads();
+        if (tid == 0 && host_flag) {   // the mean is in U1[i+1] (stream-ordered for the next slice)
+            __threadfence();
+            __hip_atomic_store(host_flag, hm_hit + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 template <int K>
@@ -686,7 +747,7 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
     const double *__restrict__ Y, int d, const double *__restrict__ q, int32_t *__restrict__ idx_out,
     double *__restrict__ dist_out, double *__restrict__ ymT, double *__restrict__ D2,
     double *__restrict__ kd2, const int32_t *__restrict__ spec_idx, int32_t *__restrict__ hit_flag,
-    int xs_doubles, const int32_t *__restrict__ spec2_idx, int32_t *host_flag) {
+    int xs_doubles, const int32_t *__restrict__ spec2_idx, int32_t *host_flag, HitMean hm) {
     __shared__ SelShm sh;
     const int qy = blockIdx.y;
     dist += (size_t)qy * rows;
@@ -697,7 +758,7 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
     if (D2) D2 += (size_t)qy * m * m;
     if (kd2) kd2 += (size_t)qy * m;
     knn_select_dev<K, false>(sh, dist, rows, m, X, Y, d, q, idx_out, dist_out, ymT, D2, kd2, spec_idx, hit_flag,
-                      xs_doubles, spec2_idx, host_flag);
+                      xs_doubles, spec2_idx, host_flag, nullptr, hm.out ? &hm : nullptr);
 }
 
 // D2 / kd2 of the selected rows by one thread per pair (pw_sqdiff, reading X): the select's former
@@ -1445,6 +1506,67 @@ __global__ void __launch_bounds__(WGT<MAXM>::T) gp_mean_kernel(NMArgs a) {
     gp_mean_dev<MAXM>(a, blockIdx.x, true);
 }
 
+// The query-independent half of gp_mean_dev for every coordinate of a speculative batch's
+// predictions (blockIdx.y = prediction, batched offsets as the fits kernels): the first arg-min
+// over the prediction's fits, then gp_mean_prep.  AP[q][c] = alpha rows 0..MAXM-1 | c | psy | ok
+// (HM_STRIDE(MAXM) doubles); pre_done[q] counts the finished workgroups.  A sweep slice whose
+// ordered list hits this prediction finishes its mean in the select kernel (knn_select_dev's
+// HitMean) from these values and its own kd2 -- bitwise gp_mean_dev, which computes the same
+// arg-min and prep on the same D2, y and fits.
+template <int MAXM>
+__global__ void __launch_bounds__(WGT<MAXM>::T) gp_pre_kernel(NMArgs a, double *__restrict__ AP,
+                                                              int32_t *__restrict__ pre_done) {
+    constexpr int RPL = GP<MAXM>::RPL, IMG = GP<MAXM>::IMG;
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    nm_batch_offsets(a);
+    const int m = a.m, d = a.d;
+    double *sD2 = sm, *sK = sm + m * m;
+    const int tid = threadIdx.x, g = tid / 16, l = tid % 16;
+    for (int i = tid; i < m * m; i += blockDim.x) sD2[i] = a.D2[i];
+    __syncthreads();
+    const int c = blockIdx.x * (blockDim.x / 16) + g;
+    const bool valid = c < d;
+    const int cc = valid ? c : 0;
+    double y[RPL];
+#pragma unroll
+    for (int s = 0; s < RPL; s++) {
+        const int row = l + 16 * s;
+        y[s] = (valid && row < m) ? a.Y[(int64_t)cc * a.ys_c + (int64_t)row * a.ys_r] : 0.0;
+    }
+    const int nfc = a.nj * a.R;
+    const double *F = a.fits_out + (size_t)4 * cc * nfc;
+    uint64_t bk = ~0ull;   // gp_mean_dev's arg-min
+    int bi = -1;
+    for (int t = l; t < nfc; t += 16) key_take(bk, bi, fval_key(F[4 * t + 2]), t);
+    row_key_min(bk, bi);
+    const double f0 = F[2];
+    const int best = (f0 != f0) ? 0 : bi;
+    const double sx = F[4 * best], sy = F[4 * best + 1];
+    const int jidx = best / a.R;
+    GPLane<MAXM> P;
+    gp_lane_init<MAXM>(P, m, l);
+    double *Kimg = sK + (size_t)g * IMG;
+    gp_image_init<MAXM>(Kimg, m, l);
+    double alpha[RPL], cq, psy;
+    const bool ok = gp_mean_prep<MAXM>(m, l, P, sD2, sx, sy, jit_lookup(a, jidx), y, Kimg, alpha, cq, psy);
+    if (valid) {
+        double *ap = AP + ((int64_t)blockIdx.y * d + c) * HM_STRIDE(MAXM);
+#pragma unroll
+        for (int s = 0; s < RPL; s++)
+            if (l + 16 * s < MAXM) ap[l + 16 * s] = alpha[s];
+        if (l == 0) {
+            ap[MAXM] = cq;
+            ap[MAXM + 1] = psy;
+            ap[MAXM + 2] = ok ? 1.0 : 0.0;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {   // the workgroup's coordinates are visible device-wide before they are counted
+        __threadfence();
+        __hip_atomic_fetch_add(pre_done + blockIdx.y, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Fused correction chain (reference parareal.py:359-382): the speculative
 // sweep's per-slice hit path as ONE persistent kernel.  For i = i0, i0+1, ...:
@@ -1994,7 +2116,7 @@ extern "C" int nngp_knn(const double *X, int64_t rows, int d, const double *q, i
     NNGP_LAUNCH_CHECK();
     launch_knn_select(dim3(1), 0, st, dist, rows, m, X, (const double *)nullptr, d, q, idx_out, dist_out,
                       (double *)nullptr, (double *)nullptr, (double *)nullptr, (const int32_t *)nullptr,
-                      (int32_t *)nullptr, 0, (const int32_t *)nullptr, (int32_t *)nullptr);
+                      (int32_t *)nullptr, 0, (const int32_t *)nullptr, (int32_t *)nullptr, HitMean{});
     NNGP_LAUNCH_CHECK();
     return NNGP_OK;
 }
@@ -2063,9 +2185,10 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
                  double fatol, double xatol, int maxfev, double *preds_out, const double *bias,
                  double *out, double *fits_out, const int32_t *spec_idx, const double *spec_fits,
                  int32_t *hit_flag, const int32_t *spec2_idx, const double *spec2_fits, int32_t *host_flag,
-                 hipStream_t st, int c0, int c1, const int32_t *wait_done, int32_t *wait_err, int phase) {
+                 hipStream_t st, int c0, int c1, const int32_t *wait_done, int32_t *wait_err, int phase,
+                 const HitMean *hm) {
     NNGP_REQUIRE(X && Y && new_x && theta0 && preds_out, "null array argument");
-    NNGP_REQUIRE(phase >= PREDICT_ALL && phase <= PREDICT_MEAN, "bad predict phase %d", phase);
+    NNGP_REQUIRE(phase >= PREDICT_ALL && phase <= PREDICT_SELECT_ONLY, "bad predict phase %d", phase);
     if (c1 < 0) c1 = d;
     NNGP_REQUIRE(0 <= c0 && c0 < c1 && c1 <= d, "bad coordinate range [%d, %d) of d=%d", c0, c1, d);
     NNGP_REQUIRE(m >= 1 && m <= MAX_M, "need 1 <= m <= %d (got %d)", MAX_M, m);
@@ -2088,17 +2211,20 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
     double *ymT = kd2 + m;
     int32_t *idx = (int32_t *)(ymT + (size_t)d * m);
     double *fits_ws = (double *)(ws + sizeof(double) * nd + sizeof(int32_t) * 64);
-    if (phase == PREDICT_ALL || phase == PREDICT_SELECT) {
-        hipLaunchKernelGGL(knn_dist_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, X, rows,
-                           d, new_x, dist);
-        NNGP_LAUNCH_CHECK();
+    if (phase == PREDICT_ALL || phase == PREDICT_SELECT || phase == PREDICT_SELECT_ONLY) {
+        if (phase != PREDICT_SELECT_ONLY) {   // (SELECT_ONLY: gdist wrote the distances)
+            hipLaunchKernelGGL(knn_dist_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, X, rows,
+                               d, new_x, dist);
+            NNGP_LAUNCH_CHECK();
+        }
         const bool wave_d2 = d2_by_waves(m, d), pair_d2 = d2_by_pairs(m, d);
         const bool sel_d2 = !wave_d2 && !pair_d2;
         launch_knn_select(dim3(1), knn_xs_bytes(m, d), st, dist, rows, m, X, Y, d, new_x, idx, (double *)nullptr,
                           ymT, sel_d2 ? D2 : (double *)nullptr, sel_d2 ? kd2 : (double *)nullptr,
                           spec ? spec_idx : (const int32_t *)nullptr,
                           spec ? hit_flag : (int32_t *)nullptr, knn_xs_doubles(m, d),
-                          spec ? spec2_idx : (const int32_t *)nullptr, spec ? host_flag : (int32_t *)nullptr);
+                          spec ? spec2_idx : (const int32_t *)nullptr, spec ? host_flag : (int32_t *)nullptr,
+                          (spec && host_flag && hm && sel_d2 && kd2) ? *hm : HitMean{});
         NNGP_LAUNCH_CHECK();
         if (wave_d2) {
             hipLaunchKernelGGL(d2_wave_kernel, dim3((unsigned)(m * (m + 1) / 2 + m)), dim3(64), 0, st, X, idx, m,
@@ -2109,7 +2235,7 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
                                idx, m, d, new_x, D2, kd2);
             NNGP_LAUNCH_CHECK();
         }
-        if (phase == PREDICT_SELECT) return NNGP_OK;
+        if (phase != PREDICT_ALL) return NNGP_OK;
     }
     // coordinates [c0, c1) only (the multi-rank sweep's share): the fits and means of those
     // columns, in the same product(coord, jitter, restart) order with their own theta0 draws
@@ -2157,6 +2283,20 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
     return run_mean(a, st);
 }
 
+// gp_pre_kernel over nq predictions of a batch (p: the batch's fits arguments with its per-prediction
+// strides): the query-independent half of every coordinate's mean, for the sweep's select to finish
+static int run_pre(const NMArgs &p, double *AP, int32_t *pre_done, int nq, hipStream_t st) {
+    const int maxm = maxm_for(p.m);
+    const int threads = wg_threads(maxm), per = threads / 16;
+    const size_t lds = sizeof(double) * ((size_t)p.m * p.m + (size_t)per * k_image_doubles(maxm));
+    const dim3 grid((unsigned)((p.d + per - 1) / per), (unsigned)nq);
+    return with_maxm(p.m, [&](auto mc) {
+        hipLaunchKernelGGL(gp_pre_kernel<decltype(mc)::value>, grid, dim3(threads), lds, st, p, AP, pre_done);
+        NNGP_LAUNCH_CHECK();
+        return NNGP_OK;
+    });
+}
+
 // The speculative batch: for nq guessed queries Q[nq][d] at once, the ordered kNN lists
 // (idx_out[nq][m]) and every fit of every prediction (fits_out[nq][n_fits][4]), with each
 // prediction's own theta0 draws (theta0[nq][n_fits][2]).  One kNN-distance launch, one
@@ -2165,7 +2305,7 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
 int spec_batch(const double *X, const double *Y, int64_t rows, int d, const double *Q, int nq, int m,
                int n_jitter, const double *jitter_exp_host, int n_restarts, const double *theta0,
                double fatol, double xatol, int maxfev, int32_t *idx_out, double *fits_out, bool latency,
-               hipStream_t st, int slot, int32_t *done, hipEvent_t ev_select) {
+               hipStream_t st, int slot, int32_t *done, hipEvent_t ev_select, double *pre_AP, int32_t *pre_done) {
     NNGP_REQUIRE(nq >= 1 && m >= 1 && m <= MAX_M && m <= rows, "bad speculative batch shape");
     NMArgs a{};
     int rc = fill_jitters(a, n_jitter, jitter_exp_host);
@@ -2179,6 +2319,7 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
     double *D2 = dist + (size_t)nq * rows;
     double *ymT = D2 + (size_t)nq * m * m;
     if (done) NNGP_HIP_CHECK(hipMemsetAsync(done, 0, sizeof(int32_t) * (size_t)nq, st));
+    if (pre_AP) NNGP_HIP_CHECK(hipMemsetAsync(pre_done, 0, sizeof(int32_t) * (size_t)nq, st));
     hipLaunchKernelGGL(knn_dist_kernel, dim3((unsigned)((rows + 63) / 64), (unsigned)nq), dim3(64), 0, st, X,
                        rows, d, Q, dist);
     NNGP_LAUNCH_CHECK();
@@ -2186,7 +2327,7 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
     launch_knn_select(dim3(1, (unsigned)nq), knn_xs_bytes(m, d), st, dist, rows, m, X, Y, d, Q, idx_out,
                       (double *)nullptr, ymT, (wave_d2 || pair_d2) ? (double *)nullptr : D2, (double *)nullptr,
                       (const int32_t *)nullptr, (int32_t *)nullptr, knn_xs_doubles(m, d), (const int32_t *)nullptr,
-                      (int32_t *)nullptr);
+                      (int32_t *)nullptr, HitMean{});
     NNGP_LAUNCH_CHECK();
     if (wave_d2) {
         hipLaunchKernelGGL(d2_wave_kernel, dim3((unsigned)(m * (m + 1) / 2), (unsigned)nq), dim3(64), 0, st, X,
@@ -2207,12 +2348,21 @@ int spec_batch(const double *X, const double *Y, int64_t rows, int d, const doub
     a.qs_D2 = (int64_t)m * m; a.qs_Y = (int64_t)d * m; a.qs_th = (int64_t)nfp * 2; a.qs_fits = (int64_t)nfp * 4;
     a.jmajor = env_int("NNGP_NM_JMAJOR", 1);   // (run_nm_parked; Burgers 0.328 -> 0.317 s)
     a.done = done;
+    const NMArgs p = a;   // (run_nm adjusts its copy's launch fields)
     // latency: a wave per fit (the re-speculation window the sweep waits on); else packed fits.
     // (The window on the packed or the 4-lanes kernel: Burgers 0.297 / 0.281 s against 0.221 s,
     // profiles/r05/nm_lanes/respec_shape_not_kept.txt -- the next slice waits on its slowest fit.)
-    if (latency) return run_nm_spec(a, st, nq);
-    return run_nm(a, false, st, nq, slot == 1 ? 7 : 8);
+    rc = latency ? run_nm_spec(a, st, nq) : run_nm(a, false, st, nq, slot == 1 ? 7 : 8);
+    if (rc || !pre_AP) return rc;
+    return run_pre(p, pre_AP, pre_done, nq, st);
 }
+
+int pre_target(int d, int m) {
+    const int per = wg_threads(maxm_for(m)) / 16;
+    return (d + per - 1) / per;
+}
+
+int pre_maxm(int m) { return maxm_for(m); }
 
 // ---- the fused correction chain, host side ----------------------------------------------------
 struct ChainRes {
@@ -2349,6 +2499,46 @@ int guess_chain(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t 
     const int rc = g_args(sys, g_tableau, g_step_mode, g_steps, g);
     if (rc) return rc;
     hipLaunchKernelGGL(guess_chain_kernel, dim3(1), dim3(64), 0, st, g, t, I, nq, sys->d, UF, UG, Q, gtmp);
+    NNGP_LAUNCH_CHECK();
+    return NNGP_OK;
+}
+
+// The sweep's slice head in ONE launch: G(U1[i]) -> UG1[i+1] and the query's kNN distances, which
+// both only read U1[i].  Blocks 0 .. nb-1 are knn_dist_kernel's (a row per thread), the last block
+// runs the G launch's device code (guess_chain_kernel's: a wave for Burgers, lane 0 for an ODE) --
+// bitwise the two launches it replaces, at one host launch (~7 us of host issue) less per slice.
+__global__ void __launch_bounds__(64) gdist_kernel(GArgs g, double T0, double T1, const double *__restrict__ X,
+                                                   int64_t rows, int d, const double *q, double *__restrict__ dist,
+                                                   double *ug_next) {
+    const int l = threadIdx.x;
+    if (blockIdx.x == gridDim.x - 1) {
+        if (g.gkind == 1) chain_burgers_g(g.fa, g.ept, g.order, g.lin, g.norm, l, T0, T1, g.g_steps, q, ug_next);
+        else if (l == 0) chain_lane_g(g.la, g.sys, g.order, g.lin, g.norm, T0, T1, g.g_steps, q, ug_next);
+        return;
+    }
+    const int64_t r = (int64_t)blockIdx.x * 64 + l;
+    if (r < rows) dist[r] = knn_dist_row(X, d, q, r);
+}
+
+bool gdist_supported(const nngp_system *sys, int g_step_mode) {
+    return env_int("NNGP_GDIST", 1) != 0 && g_in_kernel(sys, g_step_mode);
+}
+
+// G of slice i and its query's distances into predict_impl's workspace (the same slot-0 layout and
+// size, so the select of PREDICT_SELECT_ONLY that follows finds them)
+int gdist(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps, const double *t, int i,
+          const double *X, int64_t rows, int d, int m, int n_jitter, int n_restarts, const double *ui,
+          double *ug_next, hipStream_t st) {
+    GArgs g;
+    const int rc = g_args(sys, g_tableau, g_step_mode, g_steps, g);
+    if (rc) return rc;
+    const size_t nd = (size_t)rows + (size_t)m * m + m + (size_t)d * m;
+    const size_t n_fits = (size_t)d * n_jitter * n_restarts;
+    int err = 0;
+    double *dist = (double *)workspace(sizeof(double) * nd + sizeof(int32_t) * 64 + sizeof(double) * 4 * n_fits, &err);
+    if (err) return err;
+    hipLaunchKernelGGL(gdist_kernel, dim3((unsigned)((rows + 63) / 64 + 1)), dim3(64), 0, st, g, t[i], t[i + 1], X,
+                       rows, d, ui, dist, ug_next);
     NNGP_LAUNCH_CHECK();
     return NNGP_OK;
 }

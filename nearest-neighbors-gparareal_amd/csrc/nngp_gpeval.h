@@ -439,25 +439,54 @@ __device__ __forceinline__ double gp_nlml(int m, int l, const GPLane<MAXM> &P, c
     return (!ok || res != res) ? INFINITY : res;
 }
 
-// posterior mean K(xm, new_x)^T alpha (models.py:162-168); NaN on Cholesky failure
+// posterior mean K(xm, new_x)^T alpha (models.py:162-168); NaN on Cholesky failure.  Two parts:
+// gp_mean_prep, everything that does not depend on the query (c, psy, alpha and potrf's success),
+// and gp_mean_finish, the query's kernel row against alpha -- so a sweep can prepare a hit slice's
+// coordinates ahead (gp_pre_kernel) and finish them in its select (bitwise gp_mean: the same
+// expressions, and doubles stored and reloaded unchanged).
+template <int MAXM>
+__device__ __forceinline__ bool gp_mean_prep(int m, int l, const GPLane<MAXM> &P, const double *sD2, double sx,
+                                             double sy, double jit, const double (&y)[GP<MAXM>::RPL], double *Kimg,
+                                             double (&alpha)[GP<MAXM>::RPL], double &c, double &psy) {
+    c = -0.5 * (1 / nn_pow10(sx));
+    psy = nn_pow10(sy);
+    double diag[GP<MAXM>::RPL];
+    return gp_factor<MAXM>(m, l, P, sD2, c, psy, jit, y, Kimg, alpha, diag);
+}
+
+// rpl rows per lane (GP<MAXM>::RPL), big = GP<MAXM>::BIG (the exp variant): run-time here, so the
+// select kernel can finish a mean for any padded size without one instantiation per size
+// kd[s] = kd2 of row l + 16 s (row 0's for rows >= m)
+template <int RPLMAX>
+__device__ __forceinline__ double gp_mean_finish(int m, int l, int rpl, bool big, const double (&kd)[RPLMAX],
+                                                 double c, double psy, const double (&alpha)[RPLMAX], bool ok) {
+    double ka[RPLMAX];
+#pragma unroll
+    for (int s = 0; s < RPLMAX; s++) {
+        const double x = c * kd[s];
+        ka[s] = (psy * (big ? nn_exp_nonpos_sep(x) : nn_exp_nonpos(x))) * alpha[s];
+    }
+    // gp_rows_sum<rpl>: the lane's rows left to right, then the row butterfly
+    double p = (l < m) ? ka[0] : 0.0;
+#pragma unroll
+    for (int s = 1; s < RPLMAX; s++)
+        if (s < rpl) p = p + ((l + 16 * s < m) ? ka[s] : 0.0);
+    const double mean = row_sum(p);
+    return ok ? mean : NAN;
+}
+
 template <int MAXM>
 __device__ __forceinline__ double gp_mean(int m, int l, const GPLane<MAXM> &P, const double *sD2,
                                           const double *skd2,
                                           double sx, double sy, double jit,
                                           const double (&y)[GP<MAXM>::RPL], double *Kimg) {
     constexpr int RPL = GP<MAXM>::RPL;
-    const double c = -0.5 * (1 / nn_pow10(sx));
-    const double psy = nn_pow10(sy);
-    double alpha[RPL], diag[RPL], ka[RPL];
-    const bool ok = gp_factor<MAXM>(m, l, P, sD2, c, psy, jit, y, Kimg, alpha, diag);
+    double alpha[RPL], c, psy;
+    const bool ok = gp_mean_prep<MAXM>(m, l, P, sD2, sx, sy, jit, y, Kimg, alpha, c, psy);
+    double kd[RPL];
 #pragma unroll
-    for (int s = 0; s < RPL; s++) {
-        const int row = l + 16 * s;
-        const double x = c * skd2[row < m ? row : 0];
-        ka[s] = (psy * (GP<MAXM>::BIG ? nn_exp_nonpos_sep(x) : nn_exp_nonpos(x))) * alpha[s];
-    }
-    const double mean = gp_rows_sum<RPL>(m, l, ka);
-    return ok ? mean : NAN;
+    for (int s = 0; s < RPL; s++) kd[s] = skd2[l + 16 * s < m ? l + 16 * s : 0];
+    return gp_mean_finish<RPL>(m, l, RPL, GP<MAXM>::BIG, kd, c, psy, alpha, ok);
 }
 
 }  // namespace nngp

@@ -169,6 +169,13 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
     if (model == NNGP_MODEL_GPFULL)
         NNGP_REQUIRE(X && Y && theta0 && rows >= 1, "full-GP model arguments (X, alpha, coefficients)");
     const int64_t n_fits = (int64_t)d * n_jitter * n_restarts;
+    // G time (g_ms_out): event pairs around the G launch of every g_every-th slice, scaled to all of
+    // them (NNGP_G_TIME_EVERY, default 8; 1 = every slice).  Each event record costs the host ~3 us
+    // on a chain whose hit slices are host-bound (profiles/r05/sweep/).
+    const int g_every = std::max(1, env_int("NNGP_G_TIME_EVERY", 8));
+    const bool gdist_ok = gdist_supported(sys, g_step_mode);
+    int64_t hit_codes[5] = {0, 0, 0, 0, 0};   // host-flag codes seen (NNGP_SWEEP_STATS=1 prints them)
+    const bool ahead_on = env_int("NNGP_SWEEP_AHEAD", 1) != 0;
     hipEvent_t *ev = nullptr;
     if (g_ms_out) {
         *g_ms_out = 0.f;
@@ -202,13 +209,22 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
     const bool chained = spec && allow_chain && chain_supported(sys, g_step_mode, m);
     const bool overlap = spec && !chained && allow_overlap && env_int("NNGP_SPEC_OVERLAP", 1) != 0;
     int32_t *done = nullptr;
+    // hit means finished in the select (NNGP_HIT_MEAN, default 1; launch chain with host flags only):
+    // every prediction of the batch (AP1) and of each re-speculation window (AP2) prepared by
+    // gp_pre_kernel after its fits, pre1 / pre2 counting the prepared workgroups per slice
+    const bool hitmean = spec && !chained && W > 0 && env_int("NNGP_HIT_MEAN", 1) != 0;
+    const size_t hst = hitmean ? (size_t)d * HM_STRIDE(pre_maxm(m)) : 0;   // doubles per slice
+    double *AP1 = nullptr, *AP2 = nullptr;
+    int32_t *pre1 = nullptr, *pre2 = nullptr;
     if (spec) {
         int err = 0;
         const size_t bytes = sizeof(double) * ((size_t)nq * d + d + (size_t)nq * n_fits * 4) +
                              sizeof(int32_t) * ((size_t)nq * m + nq + nq) +
                              (W > 0 ? sizeof(double) * ((size_t)W * d + d + (size_t)nq * n_fits * 4) +
                                           sizeof(int32_t) * (size_t)nq * m
-                                    : 0);
+                                    : 0) +
+                             (hitmean ? sizeof(double) * (2 * (size_t)nq * hst + 1) + sizeof(int32_t) * 2 * (size_t)nq
+                                      : 0);
         char *ws = (char *)workspace(bytes, &err, 2);
         if (err) return err;
         double *Qg = (double *)ws;
@@ -228,6 +244,14 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
             NNGP_HIP_CHECK(hipMemsetAsync(spec2_idx, 0xFF, sizeof(int32_t) * (size_t)nq * m, st));   // -1: none
             for (int64_t j = 0; j < nq; j++) rs->hflags[j] = -1;
         }
+        if (hitmean) {   // after the int32 arrays, 8-byte aligned
+            const size_t off = ((size_t)((char *)(done + nq + (size_t)nq * m) - ws) + 7) & ~(size_t)7;
+            AP1 = (double *)(ws + off);
+            AP2 = AP1 + (size_t)nq * hst;
+            pre1 = (int32_t *)(AP2 + (size_t)nq * hst);
+            pre2 = pre1 + nq;
+            NNGP_HIP_CHECK(hipMemsetAsync(pre1, 0, sizeof(int32_t) * 2 * (size_t)nq, st));
+        }
         NNGP_HIP_CHECK(hipMemcpyAsync(Qg, U1 + (size_t)I * d, sizeof(double) * d, hipMemcpyDeviceToDevice, st));
         if (guess_chain_supported(sys, g_step_mode))   // one launch for the whole chain (bitwise)
             rc = guess_chain(sys, g_tableau, g_step_mode, g_steps, t, I, (int)nq, UF, UG, Qg, gtmp, st);
@@ -244,14 +268,14 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
             NNGP_HIP_CHECK(hipEventRecord(rs->ev_pre, st));             // the guesses Qg
             NNGP_HIP_CHECK(hipStreamWaitEvent(rs->st3, rs->ev_pre, 0));
             rc = spec_batch(X, Y, rows, d, Qg, (int)nq, m, n_jitter, jitter_exp_host, n_restarts, theta0, fatol,
-                            xatol, maxfev, spec_idx, spec_fits, false, rs->st3, 1, done, rs->ev_sel);
+                            xatol, maxfev, spec_idx, spec_fits, false, rs->st3, 1, done, rs->ev_sel, AP1, pre1);
             if (rc == NNGP_OK) {
                 NNGP_HIP_CHECK(hipEventRecord(rs->ev_b, rs->st3));
                 NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_sel, 0));   // lists ready; fits may run on
             }
         } else if (rc == NNGP_OK) {
             rc = spec_batch(X, Y, rows, d, Qg, (int)nq, m, n_jitter, jitter_exp_host, n_restarts, theta0, fatol,
-                            xatol, maxfev, spec_idx, spec_fits, false, st);
+                            xatol, maxfev, spec_idx, spec_fits, false, st, 1, nullptr, nullptr, AP1, pre1);
         }
         if (rc) return rc;
     }
@@ -302,53 +326,98 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
         if (g_ms_out && rc == NNGP_OK) *g_ms_out = g_ms;
         ev = nullptr;   // G time comes from the chain's clock
     }
-    for (int i = chained ? N : I; i < N && rc == NNGP_OK; i++) {   // the launch chain
+    // ---- the launch chain
+    auto split_at = [&](int i) { return spec && W > 0 && i + 1 < N; };
+    // with a host flag (W > 0, not the last slice) the prediction is issued in two parts: the kNN +
+    // select, then -- once the host has read the select's hit code -- the mean alone on a hit (the
+    // fits are the batch's) or the fits and the mean on a miss.  The fits launch a hit would have
+    // skipped on the device is never issued: its waves (191 VGPRs) could only be dispatched once the
+    // overlapped batch's waves drained a SIMD.  With HitMean the select finishes a hit's mean itself
+    // once the prediction is prepared (host code 3 / 4), and no mean launch follows.
+    auto predict_at = [&](int i, int phase, bool host_flag) {
+        const size_t j = (size_t)(i - I);
+        HitMean hm{};
+        if (hitmean && host_flag && split_at(i))
+            hm = HitMean{AP1 + j * hst, AP2 + j * hst, pre1 + j, pre2 + j, pre_target(d, m), pre_maxm(m),
+                         UG1 + (size_t)(i + 1) * d, U1 + (size_t)(i + 1) * d, preds_scratch};
+        return predict_impl(X, Y, rows, d, U1 + (size_t)i * d, m, n_jitter, jitter_exp_host, n_restarts,
+                            theta0 + j * n_fits * 2, fatol, xatol, maxfev, preds_scratch, UG1 + (size_t)(i + 1) * d,
+                            U1 + (size_t)(i + 1) * d, nullptr, spec ? spec_idx + j * m : nullptr,
+                            spec ? spec_fits + j * n_fits * 4 : nullptr, spec ? flags + j : nullptr,
+                            W > 0 ? spec2_idx + j * m : nullptr, W > 0 ? spec2_fits + j * n_fits * 4 : nullptr,
+                            (host_flag && split_at(i)) ? rs->hflags + j : nullptr, st, 0, -1,   // every written
+                            overlap ? done + j : nullptr, overlap ? rs->herr : nullptr, phase,  // flag is awaited
+                            hm.out ? &hm : nullptr);
+    };
+    // slice i's head: G(U1[i]) (with the kNN distances as one launch, gdist, on the untimed split
+    // slices), the re-speculation window's lists, and the select (or the whole prediction)
+    auto head = [&](int i) -> int {
+        const size_t j = (size_t)(i - I);
         const double *ui = U1 + (size_t)i * d;
         double *ug_next = UG1 + (size_t)(i + 1) * d;
         double *u_next = U1 + (size_t)(i + 1) * d;
-        const size_t j = (size_t)(i - I);
-        if (ev) NNGP_HIP_CHECK(hipEventRecord(ev[2 * j], st));
-        rc = nngp_rk_batch(sys, g_tableau, g_step_mode, 1, t + i, t + i + 1, g_steps, ui, ug_next, stream);
-        if (rc) break;
-        if (ev) NNGP_HIP_CHECK(hipEventRecord(ev[2 * j + 1], st));
-        if (model == NNGP_MODEL_PARAREAL) {   // (uF - uG_prev) + uG_new, models.py:82-83
-            rc = nngp_parareal_update(d, UF + (size_t)(i + 1) * d, UG + (size_t)(i + 1) * d, ug_next,
-                                      u_next, stream);
-            continue;
+        const bool timed = ev && j % (size_t)g_every == 0;
+        const bool fused = model == NNGP_MODEL_NNGP && split_at(i) && gdist_ok && !timed;
+        if (fused) {
+            const int r = gdist(sys, g_tableau, g_step_mode, g_steps, t, i, X, rows, d, m, n_jitter, n_restarts, ui,
+                                ug_next, st);
+            if (r) return r;
+        } else {
+            if (timed) NNGP_HIP_CHECK(hipEventRecord(ev[2 * j], st));
+            const int r = nngp_rk_batch(sys, g_tableau, g_step_mode, 1, t + i, t + i + 1, g_steps, ui, ug_next, stream);
+            if (r) return r;
+            if (timed) NNGP_HIP_CHECK(hipEventRecord(ev[2 * j + 1], st));
         }
-        if (model == NNGP_MODEL_GPFULL) {     // GPjax_p.predict + uG (models.py:456-462)
-            rc = gpfull_mean(X, rows, d, ui, theta0, Y, ug_next, u_next, st);
-            continue;
-        }
+        if (model == NNGP_MODEL_PARAREAL)   // (uF - uG_prev) + uG_new, models.py:82-83
+            return nngp_parareal_update(d, UF + (size_t)(i + 1) * d, UG + (size_t)(i + 1) * d, ug_next, u_next, stream);
+        if (model == NNGP_MODEL_GPFULL)     // GPjax_p.predict + uG (models.py:456-462)
+            return gpfull_mean(X, rows, d, ui, theta0, Y, ug_next, u_next, st);
         if (W > 0) {
-            NNGP_HIP_CHECK(hipEventRecord(rs->ev_g, st));                  // G(U1[i]) done
             if (respec_pending) NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_r, 0));   // lists/fits ready
             respec_pending = false;
         }
-        // with a host flag (W > 0, not the last slice) the prediction is issued in two parts: the
-        // kNN + select, then -- once the host has read the select's hit code -- the mean alone on a
-        // hit (the fits are the batch's) or the fits and the mean on a miss.  The fits launch a hit
-        // would have skipped on the device is never issued: its waves (191 VGPRs) could only be
-        // dispatched once the overlapped batch's waves drained a SIMD.
-        const bool split = spec && W > 0 && i + 1 < N;
-        auto predict = [&](int phase) {
-            return predict_impl(X, Y, rows, d, ui, m, n_jitter, jitter_exp_host, n_restarts, theta0 + j * n_fits * 2,
-                                fatol, xatol, maxfev, preds_scratch, ug_next, u_next, nullptr,
-                                spec ? spec_idx + j * m : nullptr, spec ? spec_fits + j * n_fits * 4 : nullptr,
-                                spec ? flags + j : nullptr, W > 0 ? spec2_idx + j * m : nullptr,
-                                W > 0 ? spec2_fits + j * n_fits * 4 : nullptr,
-                                split ? rs->hflags + j : nullptr, st, 0, -1,   // every written flag is awaited
-                                overlap ? done + j : nullptr, overlap ? rs->herr : nullptr, phase);
-        };
-        rc = predict(split ? PREDICT_SELECT : PREDICT_ALL);
-        if (rc || !split) continue;
+        return predict_at(i, split_at(i) ? (fused ? PREDICT_SELECT_ONLY : PREDICT_SELECT) : PREDICT_ALL, true);
+    };
+    // Look-ahead (HitMean only): once the batch's predictions are all prepared, a hit finishes in its
+    // select, so slice i+1's head is queued behind slice i's select before the host reads slice i's
+    // code.  On a miss or a hit that still needs the mean kernel, the early head read a U1[i+1] that
+    // was not written yet: the host waits for its select's host flag, resets it, redoes slice i's
+    // distances and select (the workspace the fits / mean read), and slice i+1's head follows later --
+    // every value the early launches wrote is written again.
+    bool pre_ready = !overlap;   // serialised batch: prepared before the sweep
+    bool issued = false;         // slice i's head was queued by slice i-1's look-ahead
+    for (int i = chained ? N : I; i < N && rc == NNGP_OK; i++) {
+        const size_t j = (size_t)(i - I);
+        if (!issued) rc = head(i);
+        issued = false;
+        if (rc) break;
+        if (model != NNGP_MODEL_NNGP || !split_at(i)) continue;
+        if (hitmean && !pre_ready) pre_ready = hipEventQuery(rs->ev_b) == hipSuccess;
+        const bool ahead = hitmean && pre_ready && ahead_on && split_at(i + 1);
+        if (ahead && (rc = head(i + 1)) != NNGP_OK) break;
         int32_t hit = 0;
         rc = wait_flag(rs->hflags + j, st, &hit);
         // a mean that gave up waiting for the overlapped batch: stop issuing, the caller reruns
         if (rc == NNGP_OK && overlap && __atomic_load_n(rs->herr, __ATOMIC_ACQUIRE) != 0) break;
-        if (rc == NNGP_OK) rc = predict(hit != 0 ? PREDICT_MEAN : PREDICT_FITS_MEAN);
+        if (rc) break;
+        // a miss's re-speculation window starts from G(U1[i]): the event is recorded only on a miss,
+        // behind the select the host has just seen finish (so behind G), before the slice's fits
+        if (hit == 0) NNGP_HIP_CHECK(hipEventRecord(rs->ev_g, st));
+        hit_codes[std::min(hit, 4)]++;
+        if (hit >= 3) {   // the select finished the mean (HitMean)
+            issued = ahead;
+            continue;
+        }
+        if (ahead) {   // undo the look-ahead (above)
+            int32_t early = 0;
+            if ((rc = wait_flag(rs->hflags + j + 1, st, &early)) != NNGP_OK) break;
+            __atomic_store_n(rs->hflags + j + 1, -1, __ATOMIC_RELEASE);
+            if ((rc = predict_at(i, PREDICT_SELECT, false)) != NNGP_OK) break;
+        }
+        rc = predict_at(i, hit != 0 ? PREDICT_MEAN : PREDICT_FITS_MEAN, true);
         if (rc || hit != 0) continue;
         // miss: re-guess slices i+1 .. i+w from the actual U1[i] on the side stream
+        double *ug_next = UG1 + (size_t)(i + 1) * d;
         const int w = (int)std::min<int64_t>(W, N - 1 - i);
         hipStream_t s2 = rs->st2;
         double *g2 = Qr + (size_t)W * d;
@@ -365,7 +434,8 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
         if (rc == NNGP_OK)   // a wave per fit: the sweep waits on this window's fits
             rc = spec_batch(X, Y, rows, d, Qr, w, m, n_jitter, jitter_exp_host, n_restarts,
                             theta0 + (j + 1) * n_fits * 2, fatol, xatol, maxfev, spec2_idx + (j + 1) * m,
-                            spec2_fits + (j + 1) * n_fits * 4, true, s2, 6);
+                            spec2_fits + (j + 1) * n_fits * 4, true, s2, 6, nullptr, nullptr,
+                            hitmean ? AP2 + (j + 1) * hst : nullptr, hitmean ? pre2 + j + 1 : nullptr);
         if (rc == NNGP_OK) {
             NNGP_HIP_CHECK(hipEventRecord(rs->ev_r, s2));
             respec_pending = true;
@@ -393,15 +463,21 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
             for (int32_t v : h) *spec_hits_out += v != 0;
         }
     }
-    if (ev && rc == NNGP_OK) {   // sum the G launches once the sweep has drained
-        NNGP_HIP_CHECK(hipEventSynchronize(ev[2 * (N - I) - 1]));
+    if (env_int("NNGP_SWEEP_STATS", 0))
+        fprintf(stderr, "sweep I=%d N=%d: miss %lld, hit (mean kernel) %lld / %lld, hit (mean in select) %lld / %lld\n",
+                I, N, (long long)hit_codes[0], (long long)hit_codes[1], (long long)hit_codes[2],
+                (long long)hit_codes[3], (long long)hit_codes[4]);
+    if (ev && rc == NNGP_OK) {   // the G launches' time once the sweep has drained
+        const int ns = (N - I - 1) / g_every + 1;   // timed slices j = 0, g_every, 2 g_every, ...
+        NNGP_HIP_CHECK(hipEventSynchronize(ev[2 * (size_t)(ns - 1) * g_every + 1]));
         float total = 0.f;
-        for (int j = 0; j < N - I; j++) {
+        for (int k = 0; k < ns; k++) {
+            const size_t j = (size_t)k * g_every;
             float ms = 0.f;
             NNGP_HIP_CHECK(hipEventElapsedTime(&ms, ev[2 * j], ev[2 * j + 1]));
             total += ms;
         }
-        *g_ms_out = total;
+        *g_ms_out = total * (float)(N - I) / (float)ns;   // every G launch of a sweep is the same work
     }
     return rc;
 }

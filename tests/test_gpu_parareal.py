@@ -166,6 +166,37 @@ def test_speculative_sweep_is_bitwise_and_hits(gpu, case, window, monkeypatch):
     assert sum(hits) > 0 and a['timings']['spec_hits'] == [0] * len(hits)
 
 
+@pytest.mark.parametrize('case', ['burgers', 'lorenz'])
+def test_sweep_host_path_variants_are_bitwise(gpu, case, monkeypatch):
+    """The sweep's host-path shortcuts against the plain launch chain, each on and all together:
+    G and the kNN distances as one launch (NNGP_GDIST), a hit's mean finished in its select from
+    coordinates prepared after the batch (NNGP_HIT_MEAN), and the look-ahead that queues the next
+    slice's head before the host reads a hit code (NNGP_SWEEP_AHEAD; undone on a miss).  Same hits,
+    every iterate bitwise.  Lorenz (chaotic) misses most slices, so the undo path runs often."""
+    if case == 'burgers':
+        ode = gpu.Burgers(d_x=128, normalization='-11')
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
+        p = gpu.Parareal(ode, s, [0, 5], 128, epsilon=5e-7, verbose=None, speculate=1)
+        kw = dict(nn=15, seed=45)
+    else:
+        ode = gpu.Lorenz(normalization='-11')
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=6, Nf=450, F='RK4', G='RK4')
+        p = gpu.Parareal(ode, s, [0, 18], 32, epsilon=5e-7, verbose=None, speculate=1)
+        kw = dict(nn=10, seed=47)
+    runs = {}
+    for name, knobs in (('plain', ('0', '0', '0')), ('gdist', ('1', '0', '0')), ('hitmean', ('0', '1', '0')),
+                        ('all', ('1', '1', '1'))):
+        for k, v in zip(('NNGP_GDIST', 'NNGP_HIT_MEAN', 'NNGP_SWEEP_AHEAD'), knobs):
+            monkeypatch.setenv(k, v)
+        runs[name] = p.run(model='nngp', **kw)
+    a = runs['plain']
+    for name, b in runs.items():
+        print(case, name, 'hits', b['timings']['spec_hits'])
+        assert a['timings']['spec_hits'] == b['timings']['spec_hits'], name
+        assert a['k'] == b['k'] and a['conv_int'] == b['conv_int'], name
+        assert np.array_equal(np.nan_to_num(a['u'], nan=7.0), np.nan_to_num(b['u'], nan=7.0)), name
+
+
 @pytest.mark.parametrize('case', ['burgers', 'hopf', 'tomlab'])
 def test_fused_guess_chain_keeps_hits_and_bits(gpu, case, monkeypatch):
     """The speculative sweep's guesses along the coarse chain by one wave (guess_chain_kernel,
