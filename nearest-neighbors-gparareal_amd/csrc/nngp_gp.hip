@@ -573,6 +573,9 @@ __device__ __forceinline__ void knn_select_dev(
                 }
             }
             s_hm = hmv;
+            // a select that finishes the mean says so on the device too (code 3 / 4): it computes no
+            // y_m / D2, so a mean kernel queued behind it (the look-ahead's form 1) must not run
+            if (hmv != 0) *hit_flag = hmv + 2;
             if (host_flag && hmv == 0) __hip_atomic_store(host_flag, hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     } else if (tid == 0) {
@@ -1425,6 +1428,8 @@ __device__ __forceinline__ void gp_mean_dev(const NMArgs &a, int blk, bool load_
     const int m = a.m, d = a.d;
     double *sD2 = sm, *skd2 = sm + m * m, *sK = skd2 + m;
     const int tid = threadIdx.x, g = tid / 16, l = tid % 16;
+    // the slice's select finished the mean itself (HitMean, hit code 3 / 4): nothing to do
+    if (a.skip && __hip_atomic_load(a.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 3) return;
     if (a.wait_done) {   // a hit served by the overlapped batch: wait for its fits of this query
         __shared__ int s_late;
         if (tid == 0) {

@@ -383,7 +383,9 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
     // code.  On a miss or a hit that still needs the mean kernel, the early head read a U1[i+1] that
     // was not written yet: the host waits for its select's host flag, resets it, redoes slice i's
     // distances and select (the workspace the fits / mean read), and slice i+1's head follows later --
-    // every value the early launches wrote is written again.
+    // every value the early launches wrote is written again.  (Before the batch is prepared, queueing
+    // slice i's mean kernel first and the head behind it measured no gain: those slices wait on the
+    // batch's fits, profiles/r05/sweep/host_path_ab.txt.)
     bool pre_ready = !overlap;   // serialised batch: prepared before the sweep
     bool issued = false;         // slice i's head was queued by slice i-1's look-ahead
     for (int i = chained ? N : I; i < N && rc == NNGP_OK; i++) {
@@ -393,7 +395,7 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
         if (rc) break;
         if (model != NNGP_MODEL_NNGP || !split_at(i)) continue;
         if (hitmean && !pre_ready) pre_ready = hipEventQuery(rs->ev_b) == hipSuccess;
-        const bool ahead = hitmean && pre_ready && ahead_on && split_at(i + 1);
+        const bool ahead = ahead_on && hitmean && pre_ready && split_at(i + 1);
         if (ahead && (rc = head(i + 1)) != NNGP_OK) break;
         int32_t hit = 0;
         rc = wait_flag(rs->hflags + j, st, &hit);
