@@ -80,7 +80,14 @@ struct HitMean {
     int maxm;                         // the padded fit size the coordinates were prepared at
     const double *bias;               // UG1[i+1]
     double *out, *preds;              // U1[i+1] = mean + bias, preds = mean
+    // profiling (NNGP_SEL_PROF=1, any select of predict_impl): wall-clock sums, relative to each
+    // launch's start, at the select's marks (rounds | merges | gathers | D2) and its end, + launches
+    uint64_t *marks;
 };
+// the select-profile buffer (uint64_t[6]) when NNGP_SEL_PROF=1, else null; sel_prof_report prints
+// and clears it (the correction sweep, at its end)
+uint64_t *sel_prof_marks();
+void sel_prof_report(const char *what);
 
 // predict_impl's launches in parts (the speculative sweep issues the select, reads its hit flag on
 // the host, and then launches the fits only on a miss): all | kNN + select | fits + mean | mean only

@@ -760,8 +760,42 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
     if (ymT) ymT += (size_t)qy * d * m;
     if (D2) D2 += (size_t)qy * m * m;
     if (kd2) kd2 += (size_t)qy * m;
+    uint64_t *mk = hm.marks;
+    if (mk && threadIdx.x == 0) {
+        const uint64_t t0 = wall_clock64();
+        for (int k = 0; k < 5; k++) mk[k] -= t0;
+        mk[5] += 1;
+    }
     knn_select_dev<K, false>(sh, dist, rows, m, X, Y, d, q, idx_out, dist_out, ymT, D2, kd2, spec_idx, hit_flag,
-                      xs_doubles, spec2_idx, host_flag, nullptr, hm.out ? &hm : nullptr);
+                      xs_doubles, spec2_idx, host_flag, mk, hm.out ? &hm : nullptr);
+    if (mk && threadIdx.x == 0) mk[4] += wall_clock64();
+}
+
+static uint64_t *g_sel_marks = nullptr;
+static int g_sel_marks_dev = -1;
+
+uint64_t *sel_prof_marks() {
+    if (env_int("NNGP_SEL_PROF", 0) == 0) return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    if (g_sel_marks_dev != dev) {
+        if (hipMalloc((void **)&g_sel_marks, 6 * sizeof(uint64_t)) != hipSuccess) return nullptr;
+        if (hipMemset(g_sel_marks, 0, 6 * sizeof(uint64_t)) != hipSuccess) return nullptr;
+        g_sel_marks_dev = dev;
+    }
+    return g_sel_marks;
+}
+
+void sel_prof_report(const char *what) {
+    uint64_t *mk = sel_prof_marks();
+    if (!mk) return;
+    uint64_t h[6] = {0, 0, 0, 0, 0, 0};
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(h, mk, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return;
+    (void)hipMemset(mk, 0, sizeof(h));
+    const double n = h[5] ? (double)h[5] : 1.0, us = 1e3 / device_wallclock_khz();
+    fprintf(stderr, "select profile %s: %llu launches, us per launch from its start: rounds %.2f merges %.2f "
+            "gathers %.2f D2/kd2 %.2f end %.2f\n", what, (unsigned long long)h[5], (int64_t)h[0] * us / n,
+            (int64_t)h[1] * us / n, (int64_t)h[2] * us / n, (int64_t)h[3] * us / n, (int64_t)h[4] * us / n);
 }
 
 // D2 / kd2 of the selected rows by one thread per pair (pw_sqdiff, reading X): the select's former
@@ -2229,7 +2263,11 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
                           spec ? spec_idx : (const int32_t *)nullptr,
                           spec ? hit_flag : (int32_t *)nullptr, knn_xs_doubles(m, d),
                           spec ? spec2_idx : (const int32_t *)nullptr, spec ? host_flag : (int32_t *)nullptr,
-                          (spec && host_flag && hm && sel_d2 && kd2) ? *hm : HitMean{});
+                          [&] {
+                              HitMean h = (spec && host_flag && hm && sel_d2 && kd2) ? *hm : HitMean{};
+                              h.marks = sel_prof_marks();
+                              return h;
+                          }());
         NNGP_LAUNCH_CHECK();
         if (wave_d2) {
             hipLaunchKernelGGL(d2_wave_kernel, dim3((unsigned)(m * (m + 1) / 2 + m)), dim3(64), 0, st, X, idx, m,

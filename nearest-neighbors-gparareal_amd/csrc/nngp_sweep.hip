@@ -465,6 +465,7 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
             for (int32_t v : h) *spec_hits_out += v != 0;
         }
     }
+    sel_prof_report("sweep");
     if (env_int("NNGP_SWEEP_STATS", 0))
         fprintf(stderr, "sweep I=%d N=%d: miss %lld, hit (mean kernel) %lld / %lld, hit (mean in select) %lld / %lld\n",
                 I, N, (long long)hit_codes[0], (long long)hit_codes[1], (long long)hit_codes[2],

@@ -45,6 +45,7 @@ KNOBS = [
     ('burgers', 'NNGP_NM_LANES_WG', '64'), ('burgers', 'NNGP_NM_LPF', '1'), ('burgers', 'NNGP_NM_LPF', '4'), ('burgers', 'NNGP_NM_LANES_FILL', '50'),
     ('burgers', 'NNGP_GDIST', '0'), ('burgers', 'NNGP_HIT_MEAN', '0'), ('burgers', 'NNGP_SWEEP_AHEAD', '0'),
     ('burgers', 'NNGP_G_TIME_EVERY', '1'), ('burgers', 'NNGP_SWEEP_STATS', '1'), ('lorenz', 'NNGP_HIT_MEAN', '0'),
+    ('burgers', 'NNGP_SEL_PROF', '1'),
 ]
 # knobs whose neutrality needs a setting these runs do not have, tested where they apply:
 # NNGP_SHARD_EMULATE_RANKS (a one-rank RCCL communicator: test_gpu_distributed.py
