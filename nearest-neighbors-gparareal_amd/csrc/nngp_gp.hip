@@ -297,23 +297,30 @@ struct SelShm {
 template <int K> __global__ void knn_select_kernel(const double *, int64_t, int, const double *, const double *, int,
                                                   const double *, int32_t *, double *, double *, double *,
                                                   double *, const int32_t *, int32_t *, int, const int32_t *,
-                                                  int32_t *, HitMean);
+                                                  int32_t *, HitMean, int);
+
+// K = 0 (rows > 4 096): up to this many rows the keys are staged once in the dynamic LDS (which
+// the launcher sizes for them; the y_m / D2 staging reuses it afterwards) instead of being re-read
+// from L2 on each of the radix passes (TomLab N = 256: ~20 of a select's ~24 us at 5 000 rows)
+static constexpr int64_t KEY_LDS_ROWS = 14336;
 
 // register-resident keys when rows <= 256*K (K = 2..16), else the streaming form (K = 0)
 template <typename... A>
 static void launch_knn_select(dim3 grid, size_t shmem, hipStream_t st, const double *dist, int64_t rows,
                               A... args) {
     const int64_t per = (rows + 255) / 256;
+    const int kl = (per > 16 && rows <= KEY_LDS_ROWS && env_int("NNGP_KEY_LDS", 1) != 0) ? 1 : 0;
+    if (kl) shmem = std::max(shmem, (size_t)rows * sizeof(uint64_t));
     if (per <= 2)
-        hipLaunchKernelGGL(knn_select_kernel<2>, grid, dim3(256), shmem, st, dist, rows, args...);
+        hipLaunchKernelGGL(knn_select_kernel<2>, grid, dim3(256), shmem, st, dist, rows, args..., kl);
     else if (per <= 4)
-        hipLaunchKernelGGL(knn_select_kernel<4>, grid, dim3(256), shmem, st, dist, rows, args...);
+        hipLaunchKernelGGL(knn_select_kernel<4>, grid, dim3(256), shmem, st, dist, rows, args..., kl);
     else if (per <= 8)
-        hipLaunchKernelGGL(knn_select_kernel<8>, grid, dim3(256), shmem, st, dist, rows, args...);
+        hipLaunchKernelGGL(knn_select_kernel<8>, grid, dim3(256), shmem, st, dist, rows, args..., kl);
     else if (per <= 16)
-        hipLaunchKernelGGL(knn_select_kernel<16>, grid, dim3(256), shmem, st, dist, rows, args...);
+        hipLaunchKernelGGL(knn_select_kernel<16>, grid, dim3(256), shmem, st, dist, rows, args..., kl);
     else
-        hipLaunchKernelGGL(knn_select_kernel<0>, grid, dim3(256), shmem, st, dist, rows, args...);
+        hipLaunchKernelGGL(knn_select_kernel<0>, grid, dim3(256), shmem, st, dist, rows, args..., kl);
 }
 
 // pw_leaf (8 <= n <= 128) on the 8 lanes of an aligned octet, lane j = lane & 7: lane j sums the
@@ -361,7 +368,7 @@ __device__ __forceinline__ void knn_select_dev(
     double *__restrict__ dist_out, double *__restrict__ ymT, double *__restrict__ D2,
     double *__restrict__ kd2, const int32_t *__restrict__ spec_idx, int32_t *__restrict__ hit_flag,
     int xs_doubles, const int32_t *__restrict__ spec2_idx, int32_t *host_flag, uint64_t *marks = nullptr,
-    const HitMean *hm = nullptr) {
+    const HitMean *hm = nullptr, bool key_lds = false) {
     // marks (profiling, thread 0's clock): after the rounds | the merges | the gathers | D2
 #define SEL_MARK(k) \
     if (marks && tid == 0) marks[k] += wall_clock64();
@@ -392,11 +399,24 @@ __device__ __forceinline__ void knn_select_dev(
     //    each of the 5 passes -- against the rounds' m passes over all rows (TomLab N = 256 late
     //    in its run: ~25 000 rows, m = 18, 172 us per select with the rounds alone).
     bool done = false;
+    // K = 0 with key_lds: the keys staged once in the dynamic LDS (KEY_LDS_ROWS)
+    extern __shared__ __attribute__((aligned(16))) double sel_dyn[];
+    uint64_t *kc = reinterpret_cast<uint64_t *>(sel_dyn);
+    if constexpr (K == 0) {
+        if (key_lds) {
+#pragma unroll 8
+            for (int r = tid; r < rows; r += 256) kc[r] = dist_key(dist[r]);
+            __syncthreads();
+        }
+    }
     auto for_keys = [&](auto &&f) {
         if constexpr (K > 0) {
 #pragma unroll
             for (int j = 0; j < K; j++)
                 if (kr[j] >= 0) f(kv[j], kr[j]);
+        } else if (key_lds) {
+#pragma unroll 8
+            for (int r = tid; r < rows; r += 256) f(kc[r], r);
         } else {
 #pragma unroll 8
             for (int r = tid; r < rows; r += 256) f(dist_key(dist[r]), r);
@@ -750,7 +770,7 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
     const double *__restrict__ Y, int d, const double *__restrict__ q, int32_t *__restrict__ idx_out,
     double *__restrict__ dist_out, double *__restrict__ ymT, double *__restrict__ D2,
     double *__restrict__ kd2, const int32_t *__restrict__ spec_idx, int32_t *__restrict__ hit_flag,
-    int xs_doubles, const int32_t *__restrict__ spec2_idx, int32_t *host_flag, HitMean hm) {
+    int xs_doubles, const int32_t *__restrict__ spec2_idx, int32_t *host_flag, HitMean hm, int key_lds) {
     __shared__ SelShm sh;
     const int qy = blockIdx.y;
     dist += (size_t)qy * rows;
@@ -767,7 +787,8 @@ __global__ void __launch_bounds__(256) knn_select_kernel(
         mk[5] += 1;
     }
     knn_select_dev<K, false>(sh, dist, rows, m, X, Y, d, q, idx_out, dist_out, ymT, D2, kd2, spec_idx, hit_flag,
-                      xs_doubles, spec2_idx, host_flag, mk, hm.out ? &hm : nullptr);
+                      xs_doubles, spec2_idx, host_flag, mk, hm.out ? &hm : nullptr,
+                      K == 0 && key_lds != 0);
     if (mk && threadIdx.x == 0) mk[4] += wall_clock64();
 }
 

@@ -212,13 +212,17 @@ def test_knn_vs_oracle(gpu, rows, d, m):
     assert np.array_equal(dist.cpu().numpy(), od)
 
 
+@pytest.mark.parametrize('key_lds', ['0', '1'])
 @pytest.mark.parametrize('rows,d,m,dups', [(30000, 3, 18, 0), (20000, 3, 64, 0), (9000, 3, 18, 400),
-                                          (4097, 2, 12, 0)])
-def test_knn_streaming_select_vs_oracle(gpu, rows, d, m, dups):
-    """rows > 4 096: the select streams its keys from memory through the radix threshold passes;
-    with `dups` copies of the query's nearest row more than SEL_CAND (256) rows tie at the threshold
-    and the m rounds take over.  Bitwise the oracle either way (ordered by distance, then row)."""
+                                          (4097, 2, 12, 0), (14336, 3, 18, 0), (14337, 3, 18, 0),
+                                          (6000, 3, 64, 300)])
+def test_knn_streaming_select_vs_oracle(gpu, rows, d, m, dups, key_lds, monkeypatch):
+    """rows > 4 096: the select streams its keys from memory through the radix threshold passes
+    (NNGP_KEY_LDS=1, the default: up to 14 336 rows from a copy staged once in LDS); with `dups`
+    copies of the query's nearest row more than SEL_CAND (256) rows tie at the threshold and the m
+    rounds take over.  Bitwise the oracle either way (ordered by distance, then row)."""
     import torch
+    monkeypatch.setenv('NNGP_KEY_LDS', key_lds)
     rng = np.random.default_rng(rows + d + dups)
     X = rng.standard_normal((rows, d))
     q = X[rows // 3] + 1e-3

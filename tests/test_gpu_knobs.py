@@ -50,7 +50,9 @@ KNOBS = [
 # knobs whose neutrality needs a setting these runs do not have, tested where they apply:
 # NNGP_SHARD_EMULATE_RANKS (a one-rank RCCL communicator: test_gpu_distributed.py
 # ::test_native_rccl_comm_and_sharded_sweep_one_rank plays 3, 7 and 8 ranks against the unsharded run)
-COVERED_ELSEWHERE = ['NNGP_SHARD_EMULATE_RANKS']
+# NNGP_KEY_LDS (selects over more than 4 096 rows: test_gpu_kernels.py
+# ::test_knn_streaming_select_vs_oracle runs every case with and without the LDS key cache)
+COVERED_ELSEWHERE = ['NNGP_SHARD_EMULATE_RANKS', 'NNGP_KEY_LDS']
 
 
 @pytest.mark.parametrize('case,knob,value', KNOBS)
