@@ -608,12 +608,29 @@ class Parareal():
         t_dev = torch.tensor(t, **f64)
         I = 0
         conv_int = []
-        u = _Ring(N + 1, n) if light else np.full((N + 1, n, N + 1), np.nan)
+        # The iterate history [N+1][n][k] and data_x / data_D [N][n][k] (parareal.py:233-246) hold
+        # one column per iteration.  They are allocated for 16 iterations and doubled when a run
+        # needs more: the reference's np.empty((N+1, n, N+1)) is 1.7 GB each at FHN-PDE d = 800,
+        # N = 512, whose runs converge in K = 2.  The returned slices [..., :k+1] are the same values.
+        cap0 = min(N + 1, 16)
+        u = _Ring(N + 1, n) if light else np.full((N + 1, n, cap0), np.nan)
         err = np.full((N + 1, N), np.nan)
         x = np.zeros((0, n))
         D = np.zeros((0, n))
-        data_x = None if light else np.full((N, n, N), np.nan)
-        data_D = None if light else np.full((N, n, N), np.nan)
+        data_x = None if light else np.full((N, n, cap0), np.nan)
+        data_D = None if light else np.full((N, n, cap0), np.nan)
+
+        def ensure_cols(c):   # history columns 0 .. c-1 exist
+            nonlocal u, data_x, data_D
+            if light or u.shape[2] >= c:
+                return
+            cap = min(N + 1, max(c, 2 * u.shape[2]))
+
+            def grown(a):
+                b = np.full(a.shape[:2] + (cap,), np.nan)
+                b[..., :a.shape[2]] = a
+                return b
+            u, data_x, data_D = grown(u), grown(data_x), grown(data_D)
         last = 0   # the column of u holding the newest iterate
         G_time = F_time = F_time_serial = 0.0
 
@@ -636,6 +653,7 @@ class Parareal():
         else:   # continue from a store_int checkpoint (parareal.py:141-209, 279-297)
             kc = int(_resume['k'])
             I, conv_int = int(_resume['I']), [int(c) for c in _resume['conv_int']]
+            ensure_cols(kc + 2)
             u[:, :, :kc + 2] = _resume['u']
             err[:, :kc + 1] = _resume['err']
             x, D = np.array(_resume['x']), np.array(_resume['D'])
@@ -659,6 +677,7 @@ class Parareal():
         k = k_start
         th_pin = None   # pinned host staging of the initial-theta draws (async upload)
         for k in range(k_start, N):
+            ensure_cols(k + 2)   # this iteration writes u[..., k + 1] and data_x / data_D[..., k]
             if verbose == 'v':
                 print(f'{self.ode_name} {model.name} iteration number (out of {N}): {k + 1} ')
             e0 = ev.start()
