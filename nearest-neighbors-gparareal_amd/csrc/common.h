@@ -95,6 +95,7 @@ enum { PREDICT_ALL = 0, PREDICT_SELECT = 1, PREDICT_FITS_MEAN = 2, PREDICT_MEAN 
 // the slice head G(U1[i]) + the query's distances as one launch (gdist_kernel): PREDICT_SELECT_ONLY
 // then launches the select alone.  gdist_supported: systems with an in-kernel G (NNGP_GDIST=0: off)
 bool gdist_supported(const nngp_system *sys, int g_step_mode);
+bool g_side_supported(const nngp_system *sys, int g_step_mode);
 int gdist(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps, const double *t, int i,
           const double *X, int64_t rows, int d, int m, int n_jitter, int n_restarts, const double *ui,
           double *ug_next, hipStream_t st);
@@ -104,7 +105,8 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
                  double *out, double *fits_out, const int32_t *spec_idx, const double *spec_fits,
                  int32_t *hit_flag, const int32_t *spec2_idx, const double *spec2_fits, int32_t *host_flag,
                  hipStream_t st, int c0 = 0, int c1 = -1, const int32_t *wait_done = nullptr,
-                 int32_t *wait_err = nullptr, int phase = PREDICT_ALL, const HitMean *hm = nullptr);
+                 int32_t *wait_err = nullptr, int phase = PREDICT_ALL, const HitMean *hm = nullptr,
+                 hipEvent_t bias_ready = nullptr);
 int gpfull_mean(const double *X, int64_t rows, int d, const double *q, const double *coef, const double *alpha,
                 const double *bias, double *out, hipStream_t st);
 int spec_batch(const double *X, const double *Y, int64_t rows, int d, const double *Q, int nq, int m,

@@ -2246,7 +2246,7 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
                  double *out, double *fits_out, const int32_t *spec_idx, const double *spec_fits,
                  int32_t *hit_flag, const int32_t *spec2_idx, const double *spec2_fits, int32_t *host_flag,
                  hipStream_t st, int c0, int c1, const int32_t *wait_done, int32_t *wait_err, int phase,
-                 const HitMean *hm) {
+                 const HitMean *hm, hipEvent_t bias_ready) {
     NNGP_REQUIRE(X && Y && new_x && theta0 && preds_out, "null array argument");
     NNGP_REQUIRE(phase >= PREDICT_ALL && phase <= PREDICT_SELECT_ONLY, "bad predict phase %d", phase);
     if (c1 < 0) c1 = d;
@@ -2323,18 +2323,24 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
             a.wait_ticks = (uint64_t)(us * device_wallclock_khz() / 1e3);
         }
     }
+    // bias_ready: the bias (UG1[i+1] = G(U1[i])) comes from another stream; the mean waits for it
+    auto mean = [&](NMArgs &ma) -> int {
+        if (bias_ready) NNGP_HIP_CHECK(hipStreamWaitEvent(st, bias_ready, 0));
+        return run_mean(ma, st);
+    };
     if (phase == PREDICT_MEAN) {   // the select's hit is known: the fits are the speculative batch's
         NNGP_REQUIRE(spec, "predict: the mean-only phase needs the speculative fits");
-        return run_mean(a, st);
+        return mean(a);
     }
     if (use_spec(a.n_fits, a.m)) {   // fits (a wave each), then arg-min + mean (+ bias) per coordinate
         rc = run_nm_spec(a, st);
         if (rc) return rc;
-        return run_mean(a, st);
+        return mean(a);
     }
     if (!spec && nm_park_cap() == 0) {
         NMArgs fu = a;
         fu.fits_out = fits_out;
+        if (bias_ready) NNGP_HIP_CHECK(hipStreamWaitEvent(st, bias_ready, 0));   // (the mean is in the fits)
         rc = run_nm(fu, true, st);
         if (rc != NNGP_E_UNSUPPORTED) return rc;
     }
@@ -2344,7 +2350,7 @@ int predict_impl(const double *X, const double *Y, int64_t rows, int d, const do
     u.preds = nullptr; u.out = nullptr; u.bias = nullptr;
     rc = run_nm_parked(u, st);
     if (rc) return rc;
-    return run_mean(a, st);
+    return mean(a);
 }
 
 // gp_pre_kernel over nq predictions of a batch (p: the batch's fits arguments with its per-prediction
@@ -2586,6 +2592,13 @@ __global__ void __launch_bounds__(64) gdist_kernel(GArgs g, double T0, double T1
 
 bool gdist_supported(const nngp_system *sys, int g_step_mode) {
     return env_int("NNGP_GDIST", 1) != 0 && g_in_kernel(sys, g_step_mode);
+}
+
+// G on a side stream beside a slice's prediction (the systems without an in-kernel G: the PDE field
+// kernels, whose one-slice G is tens of microseconds -- FHN-PDE d = 800: ~75 us of a ~1.8 ms
+// correction); NNGP_G_SIDE=0: on the sweep's stream
+bool g_side_supported(const nngp_system *sys, int g_step_mode) {
+    return env_int("NNGP_G_SIDE", 1) != 0 && !g_in_kernel(sys, g_step_mode);
 }
 
 // G of slice i and its query's distances into predict_impl's workspace (the same slot-0 layout and

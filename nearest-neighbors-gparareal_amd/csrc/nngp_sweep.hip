@@ -90,6 +90,32 @@ static int respec_resources(size_t nflags, Respec **out) {
     return NNGP_OK;
 }
 
+// G beside the prediction (g_side_supported): a side stream and its two ordering events
+struct GSide {
+    int dev = -1;
+    hipStream_t st = nullptr;
+    hipEvent_t ev_u = nullptr, ev_g = nullptr;   // U1[i] ready (sweep stream) / G(U1[i]) done (side)
+};
+static GSide g_gside;
+
+static int gside_resources(GSide **out) {
+    std::lock_guard<std::mutex> lk(g_respec_mu);
+    int dev = 0;
+    NNGP_HIP_CHECK(hipGetDevice(&dev));
+    if (g_gside.dev != dev) {
+        if (g_gside.st) (void)hipStreamDestroy(g_gside.st);
+        for (hipEvent_t e : {g_gside.ev_u, g_gside.ev_g})
+            if (e) (void)hipEventDestroy(e);
+        g_gside = GSide{};
+        NNGP_HIP_CHECK(hipStreamCreateWithFlags(&g_gside.st, hipStreamNonBlocking));
+        NNGP_HIP_CHECK(hipEventCreateWithFlags(&g_gside.ev_u, hipEventDisableTiming));
+        NNGP_HIP_CHECK(hipEventCreateWithFlags(&g_gside.ev_g, hipEventDisableTiming));
+        g_gside.dev = dev;
+    }
+    *out = &g_gside;
+    return NNGP_OK;
+}
+
 // nngp_shutdown: the side streams, events and host-mapped flags (re-created on next use)
 void sweep_release() {
     events_release();
@@ -102,6 +128,10 @@ void sweep_release() {
     if (r.herr) (void)hipHostFree(r.herr);
     if (r.hflags) (void)hipHostFree(r.hflags);
     r = Respec{};
+    if (g_gside.st) (void)hipStreamDestroy(g_gside.st);
+    for (hipEvent_t e : {g_gside.ev_u, g_gside.ev_g})
+        if (e) (void)hipEventDestroy(e);
+    g_gside = GSide{};
 }
 
 // wait for the select kernel's host-mapped hit flag (-1 = not yet written); a stream that has
@@ -174,6 +204,11 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
     // on a chain whose hit slices are host-bound (profiles/r05/sweep/).
     const int g_every = std::max(1, env_int("NNGP_G_TIME_EVERY", 8));
     const bool gdist_ok = gdist_supported(sys, g_step_mode);
+    GSide *gs = nullptr;
+    if (model == NNGP_MODEL_NNGP && g_side_supported(sys, g_step_mode)) {
+        const int rc0 = gside_resources(&gs);
+        if (rc0) return rc0;
+    }
     int64_t hit_codes[5] = {0, 0, 0, 0, 0};   // host-flag codes seen (NNGP_SWEEP_STATS=1 prints them)
     const bool ahead_on = env_int("NNGP_SWEEP_AHEAD", 1) != 0;
     hipEvent_t *ev = nullptr;
@@ -334,7 +369,7 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
     // skipped on the device is never issued: its waves (191 VGPRs) could only be dispatched once the
     // overlapped batch's waves drained a SIMD.  With HitMean the select finishes a hit's mean itself
     // once the prediction is prepared (host code 3 / 4), and no mean launch follows.
-    auto predict_at = [&](int i, int phase, bool host_flag) {
+    auto predict_at = [&](int i, int phase, bool host_flag, hipEvent_t bias_ready = nullptr) {
         const size_t j = (size_t)(i - I);
         HitMean hm{};
         if (hitmean && host_flag && split_at(i))
@@ -347,7 +382,7 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
                             W > 0 ? spec2_idx + j * m : nullptr, W > 0 ? spec2_fits + j * n_fits * 4 : nullptr,
                             (host_flag && split_at(i)) ? rs->hflags + j : nullptr, st, 0, -1,   // every written
                             overlap ? done + j : nullptr, overlap ? rs->herr : nullptr, phase,  // flag is awaited
-                            hm.out ? &hm : nullptr);
+                            hm.out ? &hm : nullptr, bias_ready);
     };
     // slice i's head: G(U1[i]) (with the kNN distances as one launch, gdist, on the untimed split
     // slices), the re-speculation window's lists, and the select (or the whole prediction)
@@ -358,10 +393,18 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
         double *u_next = U1 + (size_t)(i + 1) * d;
         const bool timed = ev && j % (size_t)g_every == 0;
         const bool fused = model == NNGP_MODEL_NNGP && split_at(i) && gdist_ok && !timed;
+        // an unsplit prediction's G on the side stream: only the mean needs G(U1[i]) (its bias)
+        const bool side = model == NNGP_MODEL_NNGP && !split_at(i) && gs && !timed;
         if (fused) {
             const int r = gdist(sys, g_tableau, g_step_mode, g_steps, t, i, X, rows, d, m, n_jitter, n_restarts, ui,
                                 ug_next, st);
             if (r) return r;
+        } else if (side) {
+            NNGP_HIP_CHECK(hipEventRecord(gs->ev_u, st));   // U1[i] (the previous slice's mean)
+            NNGP_HIP_CHECK(hipStreamWaitEvent(gs->st, gs->ev_u, 0));
+            const int r = nngp_rk_batch(sys, g_tableau, g_step_mode, 1, t + i, t + i + 1, g_steps, ui, ug_next, gs->st);
+            if (r) return r;
+            NNGP_HIP_CHECK(hipEventRecord(gs->ev_g, gs->st));
         } else {
             if (timed) NNGP_HIP_CHECK(hipEventRecord(ev[2 * j], st));
             const int r = nngp_rk_batch(sys, g_tableau, g_step_mode, 1, t + i, t + i + 1, g_steps, ui, ug_next, stream);
@@ -376,7 +419,8 @@ static int correction_sweep(const nngp_system *sys, int g_tableau, int g_step_mo
             if (respec_pending) NNGP_HIP_CHECK(hipStreamWaitEvent(st, rs->ev_r, 0));   // lists/fits ready
             respec_pending = false;
         }
-        return predict_at(i, split_at(i) ? (fused ? PREDICT_SELECT_ONLY : PREDICT_SELECT) : PREDICT_ALL, true);
+        return predict_at(i, split_at(i) ? (fused ? PREDICT_SELECT_ONLY : PREDICT_SELECT) : PREDICT_ALL, true,
+                          side ? gs->ev_g : nullptr);
     };
     // Look-ahead (HitMean only): once the batch's predictions are all prepared, a hit finishes in its
     // select, so slice i+1's head is queued behind slice i's select before the host reads slice i's

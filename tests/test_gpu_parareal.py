@@ -197,6 +197,29 @@ def test_sweep_host_path_variants_are_bitwise(gpu, case, monkeypatch):
         assert np.array_equal(np.nan_to_num(a['u'], nan=7.0), np.nan_to_num(b['u'], nan=7.0)), name
 
 
+@pytest.mark.parametrize('case', ['fhn512', 'burgers_lds'])
+def test_g_side_stream_is_bitwise(gpu, case, monkeypatch):
+    """Without speculation a PDE sweep slice's G runs on a side stream beside its kNN and fits, and
+    only the mean waits for it (NNGP_G_SIDE=1, the default): every iterate bitwise the plain chain."""
+    if case == 'fhn512':   # FHN-PDE d = 512, point-pair G
+        ode = gpu.FHN_PDE(d_x=16)
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=10, Nf=100, F='RK8', G='RK4')
+        p = gpu.Parareal(ode, s, [0, 4], 8, epsilon=5e-7, verbose=None, speculate=0)
+        kw = dict(nn=20, seed=45, early_stop=3)
+    else:                  # Burgers on the LDS field kernel (no in-kernel G)
+        monkeypatch.setenv('NNGP_BURGERS_LDS', '1')
+        ode = gpu.Burgers(d_x=128, normalization='-11')
+        s = gpu.SolverRK(ode.get_vector_field(), Ng=4, Nf=2000, F='RK8', G='RK1')
+        p = gpu.Parareal(ode, s, [0, 1.25], 32, epsilon=5e-7, verbose=None, speculate=0)
+        kw = dict(nn=15, seed=45, early_stop=3)
+    monkeypatch.setenv('NNGP_G_SIDE', '0')
+    a = p.run(model='nngp', **kw)
+    monkeypatch.setenv('NNGP_G_SIDE', '1')
+    b = p.run(model='nngp', **kw)
+    assert a['k'] == b['k'] and a['conv_int'] == b['conv_int']
+    assert np.array_equal(np.nan_to_num(a['u'], nan=7.0), np.nan_to_num(b['u'], nan=7.0))
+
+
 @pytest.mark.parametrize('case', ['burgers', 'hopf', 'tomlab'])
 def test_fused_guess_chain_keeps_hits_and_bits(gpu, case, monkeypatch):
     """The speculative sweep's guesses along the coarse chain by one wave (guess_chain_kernel,
