@@ -146,7 +146,10 @@ def fine_sweep_bench(torch, g, world, rank, steps, warmup, steps_per_slice, slic
         elapsed = float(tt.item())
     kernel_s = np.mean([a.elapsed_time(b) / 1e3 for a, b in ev])
     check = None
-    if world > 1:   # the library's RCCL all-gather on the same end states, bitwise torch's
+    if world > 1 and not g.parareal.native_comm_default():
+        check = {'nngp_allgather_states_bitwise_torch': None,
+                 'note': 'library communicator not exercised: opt-in, NNGP_NATIVE_COMM=1'}
+    elif world > 1:   # the library's RCCL all-gather on the same end states, bitwise torch's
         try:
             if g._lib.comm_for(None):
                 native = torch.full_like(gathered, float('nan'))
@@ -236,12 +239,15 @@ def published_runs(torch, g):
     return out
 
 
-def published_k_table(torch, g):
+def published_k_table(torch, g, live_extra=None):
     """The reference's published K table (tests/published_k.py: Hopf.py, FHN_PDE.py, Burgers.py on
-    the legacy driver).  Two cheap entries are run live here (Burgers T = 5.9 and FHN-PDE d_x = 10
-    classic Parareal, ~25 s together); the rest -- minutes each -- are read from the newest committed
-    profiles/rNN/published_k/*.json, written on this hardware by tools/published_k_run.py (the same
-    code the -m gpu tests run, tests/test_gpu_published_k.py)."""
+    the legacy driver).  Run live here: Burgers T = 5.9 and FHN-PDE d_x = 10 classic Parareal (~25 s
+    together) plus the rows in `live_extra` (the whole published runs main() makes: Hopf N = 128
+    nnGParareal, FHN-PDE d_x = 16 nnGParareal on the published paged schedule).  The rest -- minutes
+    each -- are read from the newest committed profiles/rNN/published_k/*.json, written on this
+    hardware by tools/published_k_run.py (the same code the -m gpu tests run,
+    tests/test_gpu_published_k.py).  Every row carries its source ('live' or the file), and the
+    exact-match counts are split the same way (exact_live, exact_recorded)."""
     import glob
     sys.path.insert(0, os.path.join(ROOT, 'tests'))
     import published_k as P
@@ -253,7 +259,9 @@ def published_k_table(torch, g):
         r = s.run(**kw)
         torch.cuda.synchronize()
         rows[name] = {'K': int(r['k']), 'published_K': pk, 'match': int(r['k']) == pk,
-                      'wall_s': time.perf_counter() - t0, 'source': 'live'}
+                      'wall_s': time.perf_counter() - t0, 'source': 'live', 'schedule': 'unpaged'}
+    for name, v in (live_extra or {}).items():
+        rows[name] = dict(v, source='live')
     dirs = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r[0-9]*', 'published_k')))
     if dirs:
         for f in sorted(glob.glob(os.path.join(dirs[-1], '*.json'))):
@@ -263,14 +271,62 @@ def published_k_table(torch, g):
             with open(f) as fh:
                 d = json.load(fh)
             rows[name] = {'K': d['K'], 'published_K': d['published_K'], 'match': d['K'] == d['published_K'],
-                          'wall_s': d['wall_s'], 'source': os.path.relpath(f, ROOT)}
+                          'wall_s': d['wall_s'], 'source': os.path.relpath(f, ROOT),
+                          'schedule': 'paged' if name.endswith('_paged') else 'unpaged'}
     det = [n for n in rows if n.split('_')[2] == 'para']
-    return {'rows': rows, 'parareal_exact': f"{sum(rows[n]['match'] for n in det)}/{len(det)}",
-            'all_exact': f"{sum(v['match'] for v in rows.values())}/{len(rows)}",
-            'note': 'name = <system>_<N>_<model>[_paged]; unpaged = Nf/N RK steps per slice; the published '
-                    'runs paged F (RK_thresh: every one of 25 / 200 pages re-uses all Nf/N steps), the same '
-                    'solution to roundoff (SURVEY.md 0.4); nnGP mismatches are epsilon straddles or within '
-                    'the seed / schedule spread (DESIGN.md 5)'}
+    live = [n for n in rows if rows[n]['source'] == 'live']
+    rec = [n for n in rows if rows[n]['source'] != 'live']
+    cnt = lambda names: f"{sum(rows[n]['match'] for n in names)}/{len(names)}"
+    return {'rows': rows, 'parareal_exact': cnt(det), 'exact_live': cnt(live), 'exact_recorded': cnt(rec),
+            'note': 'name = <system>_<N>_<model>[_paged]; unpaged = Nf/N RK steps per slice; paged = the '
+                    'published scripts\' RK_thresh schedule (every one of 25 / 200 pages re-uses all Nf/N '
+                    'steps: a 25x / 200x finer fine step). The two fine solutions differ by more than '
+                    'roundoff for the stiff / long runs (tools/paging_delta.py), and nnGParareal K can '
+                    'move with the schedule (FHN-PDE d_x = 10: 11 paged, 9 unpaged; d_x = 12: 10 / 8), so '
+                    'each row states its schedule; nnGP mismatches are discussed in DESIGN.md 5'}
+
+
+def published_live(torch, g, name, reference_wall_s=None, reference_cores=None):
+    """One row of the reference's published table run live, whole, at its published configuration
+    (tests/published_k.py builds it from the script, file:line cited there): K against the
+    published K, wall clock against the published run's where it is known."""
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    import published_k as P
+    s, kw, pk = P.build(g, name)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r = s.run(**kw)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    sm = P.summarise(r)
+    out = {'K': sm['K'], 'published_K': pk, 'match': sm['K'] == pk, 'wall_s': wall, 'converged': sm['converged'],
+           'conv_int_tail': sm['conv_int'][-6:], 'err_max': sm['err_max'], 'F_time_s': sm['F_time_s'],
+           'mdl_time_s': sm['mdl_time_s'], 'schedule': 'paged' if name.endswith('_paged') else 'unpaged',
+           'steps_per_slice_per_iteration': int(s.Nf / s.N) * (int(round(s.Nf / s.N / s.RK_thresh))
+                                                                if s.RK_thresh != float('inf') else 1)}
+    if reference_wall_s:
+        out.update({'reference_wall_s': reference_wall_s, 'reference_cores': reference_cores,
+                    'speedup_vs_reference_wall': reference_wall_s / wall})
+    log('published live', name, json.dumps({k: out[k] for k in ('K', 'published_K', 'wall_s')}))
+    return out
+
+
+def hopf_fixture_check(r):
+    """bench.py's Hopf solve against its oracle-loop fixture (tests/golden/hopf128_13m_nngp.npz,
+    tests/golden/gen_oracle_loops.py): K, conv_int and the SHA-256 of every iterate, and the final
+    state's error against the serial fine solution."""
+    import hashlib
+    path = os.path.join(ROOT, 'tests', 'golden', 'hopf128_13m_nngp.npz')
+    if not os.path.exists(path):
+        return {'fixture': None}
+    P = np.load(path)
+    a = np.ascontiguousarray(np.nan_to_num(np.asarray(r['u'], dtype=np.float64), nan=7.0))
+    dig = hashlib.sha256(a.tobytes()).hexdigest()
+    err = float(np.max(np.abs(r['u'][:, :, -1] - P['fine'])))
+    return {'fixture': os.path.relpath(path, ROOT), 'K_oracle_loop': int(P['k']),
+            'bitwise_oracle_loop': bool(dig == str(P['digest']) and r['k'] == int(P['k'])
+                                        and list(r['conv_int']) == [int(c) for c in P['conv_int']]),
+            'final_state_error_vs_serial_fine': err}
 
 
 def corrections_fhn_d200(torch, g, n_pred=20):
@@ -329,6 +385,15 @@ def _maxm(m):
     return m
 
 
+def _corr_inputs(d, m, rows=3000):
+    """Synthetic training set and query of one correction at shape (d, m): a random walk clipped to
+    the normalised box, a smooth field of it plus noise (the same inputs on the GPU and CPU legs)."""
+    rng = np.random.default_rng(d + m)
+    X = np.clip(np.cumsum(0.01 * rng.standard_normal((rows, d)), axis=0), -1, 1)
+    Y = 0.02 * np.sin(2 * X) + 1e-5 * rng.standard_normal((rows, d))
+    return X, Y, X[rows // 3] + 1e-3
+
+
 def correction_roofline(torch, g, d, m, R=1, rows=3000, reps=3):
     """Roofline of one nnGP correction (NNGP_p.predict = kNN + d*9*R Nelder-Mead fits + arg-min +
     posterior mean, models.py:171-226): algorithmic flops = sum over fits of nfev x (m^3/3 + 2m^2
@@ -336,16 +401,14 @@ def correction_roofline(torch, g, d, m, R=1, rows=3000, reps=3):
     evaluation, plus m(m+1)/2 exps counted separately -- over the correction's
     device time (HIP events on the launch stream), against the FP64 VALU peak.  The kernels run
     padded to the next instantiated size M; the executed flops at M are reported beside."""
-    rng = np.random.default_rng(d + m)
-    X = np.clip(np.cumsum(0.01 * rng.standard_normal((rows, d)), axis=0), -1, 1)
-    Y = 0.02 * np.sin(2 * X) + 1e-5 * rng.standard_normal((rows, d))
+    X, Y, qh = _corr_inputs(d, m, rows)
     dev = lambda a: torch.tensor(a, dtype=torch.float64, device='cuda')
     Xt, Yt = dev(X), dev(Y)
     mdl = g.NNGP_p(n=d, N=4, nn=m, n_restarts=R, seed=45)
     th0 = dev(mdl.draw_thetas(1))
-    q = Xt[rows // 3] + 1e-3
+    q = dev(qh)
     fits = torch.empty((mdl.n_fits, 4), dtype=torch.float64, device='cuda')
-    mdl.predict_device(Xt, Yt, rows, q, th0, fits_out=fits)
+    preds = mdl.predict_device(Xt, Yt, rows, q, th0, fits_out=fits).clone()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
@@ -361,11 +424,46 @@ def correction_roofline(torch, g, d, m, R=1, rows=3000, reps=3):
     ev = float(nfev.sum())
     tf = ev * per / sec / 1e12
     return {'d': d, 'm': m, 'R': R, 'rows': rows, 'fits': mdl.n_fits, 'ms_per_correction': sec * 1e3,
+            'corrections_per_s': 1 / sec, 'fits_per_s': mdl.n_fits / sec, 'evaluations_per_s': ev / sec,
             'evaluations': ev, 'nfev_mean': float(nfev.mean()), 'nfev_max': int(nfev.max()),
             'flops_per_evaluation': per, 'exps_per_evaluation': m * (m + 1) / 2, 'padded_to': M,
             'achieved_tflops': tf, 'frac_fp64_peak': tf / FP64_PEAK_TFLOPS,
             'executed_tflops_padded': ev * per_M / sec / 1e12,
+            '_preds': preds.cpu().numpy(),
             'note': 'latency-bound: a correction waits for its slowest fit (nfev_max evaluations in sequence)'}
+
+
+def cpu_corrections(gpu_rows, threads):
+    """BASELINE.md E.2's CPU side of the correction metric: the same corrections as
+    nngp_correction_roofline (same training set, query and theta0 draws) on the host through the
+    oracle's C restatement (oracle/nngp_oracle.c orc_predict: kNN + the d*9*R Nelder-Mead fits,
+    OpenMP over the fits, + arg-min + posterior mean) -- corrections/s and NM fits/s beside the
+    GPU's, and whether the predictions are bitwise the GPU's."""
+    O = _oracle()
+    out = {}
+    for key, gr in gpu_rows.items():
+        d, m, R, rows = gr['d'], gr['m'], gr['R'], gr['rows']
+        X, Y, q = _corr_inputs(d, m, rows)
+        nf = d * 9 * R
+        th0 = np.random.default_rng(45).integers(-8, 0, (nf, 2)).astype(np.float64)   # NNGP_p.draw_thetas(1)
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            preds = O.predict(X, Y, q, m, th0, n_restarts=R, nthreads=threads)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el > 1.0 or reps >= 20:
+                break
+        sec = el / reps
+        out[key] = {'d': d, 'm': m, 'R': R, 'fits': nf, 'cpu_ms_per_correction': sec * 1e3,
+                    'cpu_corrections_per_s': 1 / sec, 'cpu_fits_per_s': nf / sec,
+                    'gpu_corrections_per_s': gr['corrections_per_s'], 'gpu_fits_per_s': gr['fits_per_s'],
+                    'gpu_over_cpu': sec / (gr['ms_per_correction'] / 1e3),
+                    'preds_bitwise_gpu': bool(np.array_equal(preds, gr['_preds'])), 'reps': reps}
+    return {'rows': out, 'cpu_threads': threads, 'host_cpus_total': os.cpu_count(), 'cpu_model': cpu_model(),
+            'note': 'CPU = oracle C restatement (gcc -O3 -march=x86-64-v4), OpenMP over the fits on the '
+                    'threads of this process\'s CPU affinity; the reference fanned the same fits over its MPI '
+                    'pool (models.py:197-202)'}
 
 
 def gparareal_lorenz(torch, g):
@@ -801,7 +899,9 @@ def sharded_sweep_timing(torch, g, solver, td, Ufull, Xd, Yd, rows, mdl, world, 
     zeros = torch.zeros(d, dtype=torch.float64, device='cuda')
     c0, c1, chunk = shard_bounds(0, d, world, rank)
     gather = torch.zeros(world * chunk, dtype=torch.float64, device='cuda')
-    comm = world > 1 and g._lib.comm_for(None)
+    # the library's communicator only when opted in (NNGP_NATIVE_COMM=1, as Parareal); otherwise
+    # the 'native' leg is the unsharded sweep on every rank
+    comm = world > 1 and g.parareal.native_comm_default() and g._lib.comm_for(None)
 
     send = torch.zeros(chunk, dtype=torch.float64, device='cuda')
 
@@ -846,7 +946,7 @@ def sharded_sweep_timing(torch, g, solver, td, Ufull, Xd, Yd, rows, mdl, world, 
         torch.distributed.all_reduce(same, op=torch.distributed.ReduceOp.MIN)
     out['native_bitwise_python_loop'] = bool(same.item())
     out['native_path'] = ('nngp_correction_sweep_sharded (library RCCL communicator)' if comm
-                          else 'nngp_correction_sweep (one rank)')
+                          else 'nngp_correction_sweep (unsharded, every rank)')
     out['slices'] = n_sw
     return out
 
@@ -971,40 +1071,24 @@ def main():
                                                    'conv_int': tim.get('conv_int', []),
                                                    'spec_hits': tim.get('spec_hits', [])}
             log(which, 'converged', conv, 'K', k, f'{wall:.2f}s')
-        # the opt-in contracted propagator on the same two solves
-        for which in ('burgers', 'hopf'):
-            wall, k, conv, tim, _ = converge(torch, g, which, fma=True)
-            res[f'{which}_n128_to_convergence_contracted'] = {
-                'wall_s': wall, 'K': k, 'converged': conv, 'F_time_s': tim['F_time'],
-                'mdl_time_s': tim['mdl_tot_t'], 'K_exact_build': res[f'{which}_n128_to_convergence']['K']}
-            log(which, 'contracted: K', k, f'{wall:.2f}s')
+        res['hopf_n128_to_convergence'].update(hopf_fixture_check(runs['hopf']))
         res['nngp_corrections_fhn_d200'] = corrections_fhn_d200(torch, g)
         res['nngp_correction_roofline'] = {f'd{d}_m{m}_R{R}': correction_roofline(torch, g, d, m, R)
                                            for d, m, R in ((800, 20, 1), (200, 20, 1), (128, 15, 1), (3, 15, 2))}
-        log('correction roofline', json.dumps(res['nngp_correction_roofline']))
+        log('correction roofline', json.dumps({k: {a: b for a, b in v.items() if a != '_preds'}
+                                                for k, v in res['nngp_correction_roofline'].items()}))
         res['nngp_corrections_hopf_vs_reference'] = {'reference_corrections_per_s_141_cores': 44.0,
                                                       'ratio': res['nngp_corrections_per_s'] / 44.0}
         res['fhn_pde_n512_to_convergence'] = fhn_pde_converge(torch, g)
         log('fhn-pde d=800 N=512', json.dumps(res['fhn_pde_n512_to_convergence']))
-        # the published FHN-PDE run at d_x = 16 (FHN_PDE.py:27-181, FHN_scal_times_16_512_nngp):
-        # G = RK4 25 steps/slice as published; reference K = 6 in 17 849 s on 517 cores
-        r16 = fhn_pde_converge(torch, g, dx=16, ng=25)
-        # same work as the published run: FHN_PDE.py:146-161 pages every slice into 25 pages that
-        # each re-run the full 195 324-step grid (new_lib.py:57-69): 4 883 100 RK8 steps per slice
-        # per iteration against the 195 325 run here, so the F part is scaled by that ratio (the
-        # per-step cost is the same kernel's) and the model / G / driver part is kept
-        paged_ratio = 25 * 195324 / 195325
-        paged_wall = r16['wall_s'] + r16['F_time_s'] * (paged_ratio - 1)
-        r16.update({'reference_K': 6, 'reference_conv_int': [1, 2, 3, 4, 7, 512], 'reference_wall_s_517_cores': 17849.0,
-                    'wall_s_paged_equivalent': paged_wall,
-                    'speedup_vs_reference_wall_same_work': 17849.0 / paged_wall,
-                    'note': 'F unpaged here (195 325 RK8 steps/slice); the published run paged it 25x '
-                            '(4 883 100 steps/slice, SURVEY.md 0.4): wall_s_paged_equivalent = wall_s + '
-                            'F_time_s x (25 x 195 324 / 195 325 - 1), the same fine work as the reference'})
-        res['fhn_pde_d512_n512_published_config'] = r16
-        log('fhn-pde d=512 N=512 published', json.dumps(r16))
+        # two whole published runs, live: Hopf N = 128 nnGParareal (Hopf.py, K = 13 in 3 565 s on 141
+        # cores) and FHN-PDE d_x = 16 nnGParareal on the published PAGED schedule (FHN_PDE.py:146-175:
+        # 25 pages x 195 324 RK8 steps per slice per iteration, K = 6 in 17 849 s on 517 cores)
+        live = {'hopf_128_nngp': published_live(torch, g, 'hopf_128_nngp', 3565.0, 141),
+                'fhn16_512_nngp_paged': published_live(torch, g, 'fhn16_512_nngp_paged', 17849.0, 517)}
+        res['published_live'] = live
         res.update(published_runs(torch, g))
-        res['published_k'] = published_k_table(torch, g)
+        res['published_k'] = published_k_table(torch, g, live)
         log('published K', json.dumps({k: (v['K'], v['published_K']) for k, v in res['published_k']['rows'].items()}))
         log('published runs', json.dumps({k: res[k]['wall_s'] for k in ('burgers_n128_published_schedule_nngp',
                                                                          'tomlab_n256_configs_schedule_nngp')}))
@@ -1019,6 +1103,10 @@ def main():
         res['hopf_n128_published_schedule_contracted'] = hopf_published_schedule(torch, g, fma=True)
         res['fhn_pde_n512_fine_sweep'] = fhn_pde_fine_sweeps(torch, g)
         res['cpu_baseline'] = cpu_baseline(args.steps_per_slice, args.slices_per_gpu)
+        res['cpu_nngp_corrections'] = cpu_corrections(res['nngp_correction_roofline'], res['cpu_baseline']['cores'])
+        for v in res['nngp_correction_roofline'].values():
+            v.pop('_preds', None)
+        log('cpu corrections', json.dumps(res['cpu_nngp_corrections']))
         res['cpu_single_core'] = cpu_single_core()
         log('cpu single core', json.dumps(res['cpu_single_core']))
         # north-star target (>= 10x the CPU path on Burgers N=128, identical K): the CPU
@@ -1031,7 +1119,10 @@ def main():
             'gpu_to_convergence_s': conv['wall_s'], 'cpu_to_convergence_s': c_s,
             'speedup_to_convergence': c_s / conv['wall_s'], 'K_gpu': conv['K'], 'K_cpu': c_r['k'],
             'iterates_bitwise_equal': same, 'cpu_F_s': c_f, 'cpu_cores': res['cpu_baseline']['cores'],
-            'cpu_model': cpu_model(),
+            'host_cpus_total': os.cpu_count(), 'cpu_model': cpu_model(),
+            'cores_note': f"the CPU solve ran {res['cpu_baseline']['cores']} OpenMP threads (this process's CPU "
+                          f"affinity) of the {os.cpu_count()} CPUs the host reports; the ratio is against those "
+                          f"threads, not the whole host",
             'note': 'CPU = oracle C restatement (gcc -O3 -march=x86-64-v4, OpenMP over slices and fits), '
                     'F in the reference dense formulation; the whole run to convergence on both sides'}
         log('burgers cpu', json.dumps(res['burgers_n128_vs_cpu']))

@@ -276,8 +276,16 @@ int nngp_gpfull_mean(const double *X, int64_t rows, int d, const double *q, cons
  * nngp_comm_unique_id: rank 0 creates the id (NNGP_COMM_UID_BYTES bytes, HOST), the caller
  *   broadcasts it (e.g. torch.distributed.broadcast_object_list); nngp_comm_init: every rank, on
  *   its device (collective); nngp_comm_size: (ranks, rank) of the live communicator, (0, -1) if
- *   none; nngp_comm_destroy: releases it (nngp_shutdown does too).                              */
+ *   none, and NNGP_E_HIP once the watchdog has aborted it; nngp_comm_destroy: releases it
+ *   (nngp_shutdown does too); nngp_comm_available: resolves RCCL only (NNGP_OK or
+ *   NNGP_E_UNSUPPORTED) -- the every-rank check before rank 0 alone creates the id.
+ * Deadline (NNGP_COMM_TIMEOUT_S, default 600 s): nngp_comm_init is RCCL's non-blocking init polled
+ *   to the deadline -- a rank whose peers never arrive aborts (ncclCommAbort) and returns
+ *   NNGP_E_HIP; every collective is bracketed by two events that a watchdog thread checks, and one
+ *   that has not finished the deadline after its stream reached it aborts the communicator (RCCL's
+ *   kernels return, the stream drains, later calls return NNGP_E_HIP).                          */
 #define NNGP_COMM_UID_BYTES 128
+int nngp_comm_available(void);
 int nngp_comm_unique_id(void *uid_out);
 int nngp_comm_init(int nranks, int rank, const void *uid);
 int nngp_comm_size(int *nranks_out, int *rank_out);
@@ -295,16 +303,25 @@ int nngp_allgather_states(const double *send, double *recv, size_t per_rank_elem
  * coordinates (nngp_predict_range), one in-place all-gather of the predictions, and
  * U1[i+1] = preds + UG1[i+1] -- all on `stream`, no host synchronisation.  Bitwise the unsharded
  * sweep on every rank (same inputs, same theta0 draws).  gather: DEVICE [nranks*chunk] scratch.
- * No speculation (every rank would need the whole batch).
- * Check mode: with a ONE-rank communicator and NNGP_SHARD_EMULATE_RANKS=W in the environment, the
- * process plays the W ranks of the split in turn (each rank's coordinates into its gather block,
- * no collective); gather must then hold W*ceil(d/W) doubles.                                     */
+ * No speculation (every rank would need the whole batch).                                       */
 int nngp_correction_sweep_sharded(const nngp_system *sys, int g_tableau, int g_step_mode, int64_t g_steps,
                                   const double *t, int I, int N, double *U1, double *UG1, const double *X,
                                   const double *Y, int64_t rows, int m, int n_jitter,
                                   const double *jitter_exp_host, int n_restarts, const double *theta0,
                                   double fatol, double xatol, int maxfev, double *gather, float *g_ms_out,
                                   void *stream);
+
+/* Test entry (one GPU): nngp_correction_sweep_sharded on a ONE-rank communicator with this process
+ * playing the emulate_ranks >= 1 ranks of the coordinate split in turn (each rank's coordinates into
+ * its gather block, no collective).  gather_elems: the length of gather, checked against
+ * emulate_ranks * ceil(d / emulate_ranks) before any launch.                                      */
+int nngp_correction_sweep_sharded_emulated(const nngp_system *sys, int g_tableau, int g_step_mode,
+                                           int64_t g_steps, const double *t, int I, int N, double *U1,
+                                           double *UG1, const double *X, const double *Y, int64_t rows, int m,
+                                           int n_jitter, const double *jitter_exp_host, int n_restarts,
+                                           const double *theta0, double fatol, double xatol, int maxfev,
+                                           double *gather, size_t gather_elems, int emulate_ranks,
+                                           float *g_ms_out, void *stream);
 
 #ifdef __cplusplus
 }

@@ -24,8 +24,8 @@ EXPORTS = ['nngp_abi_version', 'nngp_last_error', 'nngp_device_count', 'nngp_rk_
            'nngp_rhs_batch', 'nngp_parareal_update', 'nngp_knn', 'nngp_nm_fit_batch',
            'nngp_gp_mean', 'nngp_predict', 'nngp_correction_sweep', 'nngp_gpfull_lml', 'nngp_gpfull_fit',
            'nngp_gpfull_mean', 'nngp_predict_range', 'nngp_chain_stats', 'nngp_sweep_late_reruns', 'nngp_shutdown',
-           'nngp_comm_unique_id', 'nngp_comm_init', 'nngp_comm_size', 'nngp_comm_destroy', 'nngp_allgather_states',
-           'nngp_correction_sweep_sharded']
+           'nngp_comm_available', 'nngp_comm_unique_id', 'nngp_comm_init', 'nngp_comm_size', 'nngp_comm_destroy',
+           'nngp_allgather_states', 'nngp_correction_sweep_sharded', 'nngp_correction_sweep_sharded_emulated']
 MODEL_PARAREAL, MODEL_NNGP, MODEL_GPFULL = 0, 1, 2
 
 
@@ -85,6 +85,7 @@ def lib():
     L.nngp_chain_stats.restype = i64
     L.nngp_sweep_late_reruns.argtypes = []
     L.nngp_sweep_late_reruns.restype = i64
+    L.nngp_comm_available.argtypes = []
     L.nngp_comm_unique_id.argtypes = [ctypes.c_char_p]
     L.nngp_comm_init.argtypes = [i32, i32, ctypes.c_char_p]
     L.nngp_comm_size.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
@@ -93,6 +94,8 @@ def lib():
     L.nngp_correction_sweep_sharded.argtypes = [ctypes.POINTER(CSystem), i32, i32, i64, _vp, i32, i32, _vp, _vp,
                                                 _vp, _vp, i64, i32, i32, _dp, i32, _vp, dbl, dbl, i32, _vp,
                                                 ctypes.POINTER(ctypes.c_float), _vp]
+    L.nngp_correction_sweep_sharded_emulated.argtypes = (L.nngp_correction_sweep_sharded.argtypes[:-2] +
+                                                         [ctypes.c_size_t, i32, ctypes.POINTER(ctypes.c_float), _vp])
     L.nngp_predict_range.argtypes = [_vp, _vp, i64, i32, _vp, i32, i32, _dp, i32, _vp, i32, i32, dbl, dbl, i32,
                                      _vp, _vp]
     for name in EXPORTS:
@@ -173,13 +176,16 @@ def comm_for(group=None):
     `group`, created once per group: rank 0 makes the unique id, torch broadcasts it, every rank
     joins on its current device.  Returns True when the native collectives are live for `group`;
     False for a gloo group (ranks sharing one GPU: RCCL refuses duplicate devices) or when RCCL
-    cannot be loaded on some rank -- the caller then keeps torch.distributed's collectives.
+    cannot be loaded, or the init fails, on some rank -- the caller then keeps torch.distributed's
+    collectives.  Collective: every rank of `group` must call it together.
 
-    The ranks agree before the collective init (every rank must be able to resolve RCCL) and after
-    it (every rank's init succeeded), so one failing rank never leaves the others blocked in RCCL.
-    The cache holds the group object itself (its id() cannot be re-used while it is held) and is
-    re-checked against nngp_comm_size, so a communicator released by nngp_shutdown /
-    nngp_comm_destroy is created again."""
+    Every decision is a MIN all-reduce over the ranks, so they all take the same branch:
+    - the cache (this group's communicator is live on this rank) -- a rank that released its
+      communicator (nngp_shutdown / nngp_comm_destroy) makes every rank re-create it;
+    - RCCL resolvable on every rank (nngp_comm_available) and rank 0's id created: only rank 0
+      calls nngp_comm_unique_id, which starts RCCL's bootstrap listener;
+    - every rank's init succeeded (nngp_comm_init: non-blocking init with a deadline,
+      NNGP_COMM_TIMEOUT_S, so a missing peer ends in an error on that rank, not a hang)."""
     import torch
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_backend(group) != 'nccl':
@@ -188,27 +194,39 @@ def comm_for(group=None):
     gobj = group if group is not None else dist.group.WORLD
     key = (id(gobj), world, rank)
     L = lib()
-    if _comm_state['key'] == key and _comm_state['group'] is gobj:
-        nr, rk = ctypes.c_int(0), ctypes.c_int(-1)
-        L.nngp_comm_size(ctypes.byref(nr), ctypes.byref(rk))
-        if (nr.value, rk.value) == (world, rank):
-            return True
-    _comm_state.update(group=None, key=None)
 
     def agree(ok):   # MIN over the group's ranks
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device='cuda')
+        flag = torch.tensor([int(ok)], dtype=torch.int32, device='cuda')
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
-        return int(flag.item()) == 1
+        return int(flag.item())
 
+    # 1: this group's communicator is live here; 0: not created / released; -1: the watchdog
+    # aborted it (a collective ran past the deadline, so results since then are void) -> raise
+    state = 0
+    if _comm_state['key'] == key and _comm_state['group'] is gobj:
+        nr, rk = ctypes.c_int(0), ctypes.c_int(-1)
+        rc = L.nngp_comm_size(ctypes.byref(nr), ctypes.byref(rk))
+        state = -1 if rc != 0 else int((nr.value, rk.value) == (world, rank))
+    state = agree(state)
+    if state < 0:
+        _comm_state.update(group=None, key=None)
+        raise NNGPError('the library communicator was aborted on some rank: a collective ran past '
+                        'NNGP_COMM_TIMEOUT_S (' + L.nngp_last_error().decode(errors='replace') + ')')
+    if state == 1:
+        return True
+    _comm_state.update(group=None, key=None)
+    L.nngp_comm_destroy()   # every rank starts the re-creation from no communicator
     uid = ctypes.create_string_buffer(COMM_UID_BYTES)
-    ok = L.nngp_comm_unique_id(uid) == 0   # every rank: resolves RCCL; rank 0's id is the one used
-    if not agree(ok):
+    ok = L.nngp_comm_available() == 0
+    if ok and rank == 0:
+        ok = L.nngp_comm_unique_id(uid) == 0
+    if agree(ok) != 1:
         return False
     obj = [uid.raw]
     src = 0 if group is None else dist.get_global_rank(group, 0)
     dist.broadcast_object_list(obj, src=src, group=group)
     rc = L.nngp_comm_init(world, rank, obj[0])
-    if not agree(rc == 0):
+    if agree(rc == 0) != 1:
         L.nngp_comm_destroy()
         return False
     _comm_state.update(group=gobj, key=key)

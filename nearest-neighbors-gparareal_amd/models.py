@@ -390,7 +390,8 @@ class GPjax_p(ModelAbstr):
         self.k = 0
         self.rounds = []
         # per training call: training rows and the likelihood evaluations its fits made (sum of
-        # nfev = the (rows+1)^2 matrices factored), for the measured Cholesky rate (bench.py)
+        # nfev = the (rows+1)^2 matrices factored), for the measured Cholesky rate (bench.py);
+        # sharded over ranks, a call's entry counts every rank's fits (tot_train_t stays this rank's)
         self.call_rows, self.call_evals = [], []
         self._dev = None   # (X [rows][n], alpha [n][rows], coef [n][2]) device tensors
         # multi-GPU (the reference's pool.map over the d*9 fits, models.py:386-392):
@@ -478,6 +479,14 @@ class GPjax_p(ModelAbstr):
             allf = _gather_rows(buf, group, world).cpu().numpy()[:self.n * nj]
             th, fv = np.ascontiguousarray(allf[:, :2]), np.ascontiguousarray(allf[:, 2])
             self.train_count[min(self.k, self.N - 1)] += self.n * nj - (c1 - c0) * nj   # all fits, as one rank counts them
+            # the call's evaluations over ALL ranks' fits (the gathered nfev column), consistent
+            # with train_count: bench.py's executed Cholesky rate reads these
+            total = int(allf[:, 3].astype(np.int64).sum())
+            if c1 > c0:
+                self.call_evals[-1] = total
+            else:
+                self.call_rows.append(int(X.shape[0]))
+                self.call_evals.append(total)
         temp = np.zeros((self.n, len(self.theta)))
         nj = len(JITTERS)
         for j in range(self.n):

@@ -481,17 +481,23 @@ class Parareal():
         if getattr(self, '_run_native_comm', False) and _lib.comm_for(self.process_group) and \
                 not solver.coarse_is_paged():
             world = torch.distributed.get_world_size(self.process_group)
-            if world == 1:   # NNGP_SHARD_EMULATE_RANKS: one process plays W ranks (include/nngp.h)
-                world = max(1, int(os.environ.get('NNGP_SHARD_EMULATE_RANKS', '1')))
-            chunk = (n + world - 1) // world
-            gather = torch.zeros(world * chunk, dtype=torch.float64, device=U1.device)
+            # NNGP_SHARD_EMULATE_RANKS=W on one rank: this process plays the W ranks of the split
+            # (include/nngp.h nngp_correction_sweep_sharded_emulated, a one-GPU check)
+            emulate = max(1, int(os.environ.get('NNGP_SHARD_EMULATE_RANKS', '1'))) if world == 1 else 0
+            vr = emulate or world
+            chunk = (n + vr - 1) // vr
+            gather = torch.zeros(vr * chunk, dtype=torch.float64, device=U1.device)
             cs = solver.f.csystem(U1.device)
             g_ms = ctypes.c_float(0.0)
-            _lib.check(lib.nngp_correction_sweep_sharded(
-                ctypes.byref(cs), _lib.TABLEAU[solver.G], solver.step_mode, solver.Ng, t_dev.data_ptr(), I, N,
-                U1.data_ptr(), UG1.data_ptr(), X.data_ptr(), Y.data_ptr(), int(rows), m, len(jit), jp,
-                model.n_restarts, th0.data_ptr(), float(model.fatol), float(model.xatol), model.maxfev,
-                gather.data_ptr(), ctypes.byref(g_ms), stream))
+            args = (ctypes.byref(cs), _lib.TABLEAU[solver.G], solver.step_mode, solver.Ng, t_dev.data_ptr(), I, N,
+                    U1.data_ptr(), UG1.data_ptr(), X.data_ptr(), Y.data_ptr(), int(rows), m, len(jit), jp,
+                    model.n_restarts, th0.data_ptr(), float(model.fatol), float(model.xatol), model.maxfev,
+                    gather.data_ptr())
+            if emulate:
+                _lib.check(lib.nngp_correction_sweep_sharded_emulated(*args, gather.numel(), emulate,
+                                                                      ctypes.byref(g_ms), stream))
+            else:
+                _lib.check(lib.nngp_correction_sweep_sharded(*args, ctypes.byref(g_ms), stream))
             model.train_count += nf * (N - I)
             self.spec_hits.append(0)
             return g_ms.value / 1e3

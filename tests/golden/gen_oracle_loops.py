@@ -12,6 +12,7 @@ here; the oracle is pinned to it by tests/test_oracle_golden.py.
     python tests/golden/gen_oracle_loops.py tomlab256_nngp         # TomLab N=256 to convergence
     python tests/golden/gen_oracle_loops.py burgers128_seeds       # BASELINE configs[2], seeds 0-7 + serial fine
     python tests/golden/gen_oracle_loops.py fhn800_fine            # configs[4]'s serial fine solution (~1e8 steps)
+    python tests/golden/gen_oracle_loops.py hopf128_13m_nngp       # bench.py's Hopf solve, 13.6e6 RK4 steps/slice
 """
 import hashlib
 import os
@@ -83,6 +84,26 @@ def tomlab256():
                    fatol=1e-3, xatol=1e-3, u0=so.fit([4.6722764, 5.2437205e-10, -6.4444208e-10]),
                    on_iter=None)
     return o, time.time() - t0
+
+
+def hopf128_13m():
+    """bench.py's `hopf_n128_to_convergence` (BASELINE configs[1] at Hopf.py's throughput schedule):
+    Hopf N = 128, '-11' normalisation, G = RK1 16 / F = RK4 13 600 000 steps per slice (Nf =
+    2048*85*10^4 / 128, unpaged), Hopf.py's nnGP settings (nn = 15, n_restarts = 2, fatol = xatol =
+    0.1, seed 45; Hopf.py:65-84), run to convergence; plus the serial fine solution at every slice
+    boundary (128 x 13.6e6 RK4 steps one after another) for the final-state error."""
+    so = O.System('hopf', param=(500.0,))
+    u0 = so.fit([0.1, 0.1, -20])
+    nf = 2048 * 85 * 10000 // 128
+    t0 = time.time()
+    o = O.parareal(so, [-20, 500], 128, 16, nf, 'RK1', 'RK4', epsilon=5e-7, model='nngp', nn=15, n_restarts=2,
+                   fatol=0.1, xatol=0.1, seed=45, u0=u0, on_iter=_progress('hopf128 13.6e6', t0))
+    sec = time.time() - t0
+    t = np.linspace(-20, 500, 129)
+    fine = [u0]
+    for i in range(128):
+        fine.append(so.rk(4, t[i], t[i + 1], nf, fine[-1]))
+    return o, np.array(fine), sec
 
 
 def burgers_fine(so, u0, N=128, Nf=2000, tspan=(0, 5)):
@@ -159,6 +180,13 @@ def main(which):
         o, sec = tomlab256()
         np.savez_compressed(os.path.join(HERE, f'{which}.npz'), k=o['k'], conv_int=np.array(o['conv_int']),
                             converged=o['converged'], digest=u_digest(o['u']), u_last=o['u'][:, :, -1], seconds=sec)
+    elif which == 'hopf128_13m_nngp':
+        o, fine, sec = hopf128_13m()
+        err_max = [float(np.nanmax(o['err'][:, k])) for k in range(o['k'])]
+        np.savez_compressed(os.path.join(HERE, f'{which}.npz'), k=o['k'], conv_int=np.array(o['conv_int']),
+                            converged=o['converged'], digest=u_digest(o['u']), u_last=o['u'][:, :, -1],
+                            u3=o['u'][:, :, :3], err_max=np.array(err_max), fine=fine,
+                            final_err=float(np.max(np.abs(o['u'][:, :, -1] - fine))), seconds=sec)
     elif which == 'fhn800_n512_nngp':
         o, sec = fhn800()
         rows = np.array([0, 1, 2, 3, 128, 256, 384, 510, 511, 512])

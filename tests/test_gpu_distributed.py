@@ -63,8 +63,9 @@ def test_native_rccl_comm_and_sharded_sweep_one_rank(gpu, tmp_path):
     nngp_correction_sweep_sharded (every slice's G, this rank's coordinates, the RCCL all-gather and
     u = preds + uG issued natively) -- bitwise the unsharded run, with and without the native path,
     and with the coordinate split of 3, 7 and 8 ranks played in turn by the one process
-    (NNGP_SHARD_EMULATE_RANKS: each rank's block and the partial last one land where the in-place
-    all-gather would put them).
+    (NNGP_SHARD_EMULATE_RANKS -> nngp_correction_sweep_sharded_emulated: each rank's block and the
+    partial last one land where the in-place all-gather would put them; a gather buffer shorter than
+    the split is refused before any launch).
     Several ranks need several GPUs for RCCL (the 8-GPU bench runs them); the orchestration across
     ranks is covered on gloo above."""
     out = str(tmp_path / 'comm.npz')
@@ -102,7 +103,17 @@ for W in (3, 7, 8):
     kw_, cw_, uw_ = run_case(g, "fhn", True, native=True)
     emu.append(kw_ == k0 and list(cw_) == list(c0) and same(uw_, u0))
 del os.environ["NNGP_SHARD_EMULATE_RANKS"]
+# the emulated entry checks the caller's gather length (3 ranks x 67 > 200) before launching
 ode = g.FHN_PDE(d_x=10)
+cs = ode.get_vector_field().csystem(torch.device("cuda", 0))
+buf = torch.zeros((17, 200), dtype=torch.float64, device="cuda")
+short = torch.zeros(200, dtype=torch.float64, device="cuda")
+jit = np.arange(-20, -11, dtype=float)
+rc_short = L.nngp_correction_sweep_sharded_emulated(
+    ctypes.byref(cs), 4, 0, 5, buf.data_ptr(), 0, 1, buf.data_ptr(), buf.data_ptr(), buf.data_ptr(), buf.data_ptr(),
+    16, 10, 9, jit.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), 1, buf.data_ptr(), 0.1, 0.1, 400,
+    short.data_ptr(), short.numel(), 3, None, torch.cuda.current_stream().cuda_stream)
+assert rc_short == -1 and b"gather holds" in L.nngp_last_error(), (rc_short, L.nngp_last_error())
 s = g.SolverRK(ode.get_vector_field(), Ng=5, Nf=100, F="RK8", G="RK4")
 r2 = g.Parareal(ode, s, [0, 8], 16, epsilon=5e-7, verbose=None).run(model="nngp", nn=20, seed=45, early_stop=2,
                                                                   shard_corrections=True, native_comm=False)
@@ -120,3 +131,43 @@ print("comm ok")
     R = np.load(out)
     assert len(set(R['k'].tolist())) == 1 and bool(R['same_native']) and bool(R['same_py']) and all(R['conv'])
     assert R['emulated'].tolist() == [True, True, True], R['emulated']
+
+
+@pytest.mark.timeout(120)
+def test_comm_init_without_peers_returns_in_bounded_time(gpu):
+    """The communicator's deadline (include/nngp.h, NNGP_COMM_TIMEOUT_S): a rank that joins a
+    two-rank communicator whose peer never arrives gets NNGP_E_HIP after the deadline (RCCL's
+    non-blocking init, polled, then ncclCommAbort) instead of blocking forever -- and the library
+    creates a working communicator afterwards.  Run in a child process under its own limit."""
+    code = r'''
+import ctypes, os, sys, time
+import torch
+sys.path.insert(0, os.environ["NNGP_ROOT"])
+torch.cuda.set_device(0)
+from nngp_amd import _lib
+L = _lib.lib()
+uid = ctypes.create_string_buffer(_lib.COMM_UID_BYTES)
+assert L.nngp_comm_available() == 0
+assert L.nngp_comm_unique_id(uid) == 0
+t0 = time.time()
+rc = L.nngp_comm_init(2, 0, uid.raw)
+el = time.time() - t0
+msg = L.nngp_last_error().decode()
+print("init without a peer: rc", rc, "after", round(el, 1), "s:", msg, flush=True)
+assert rc == -2 and "still waiting for its peers" in msg and el < 40, (rc, el, msg)
+nr, rk = ctypes.c_int(7), ctypes.c_int(7)
+assert L.nngp_comm_size(ctypes.byref(nr), ctypes.byref(rk)) == 0 and (nr.value, rk.value) == (0, -1)
+# a one-rank communicator works after the aborted one
+assert L.nngp_comm_unique_id(uid) == 0
+assert L.nngp_comm_init(1, 0, uid.raw) == 0, L.nngp_last_error()
+x = torch.arange(6, dtype=torch.float64, device="cuda"); y = torch.zeros(6, dtype=torch.float64, device="cuda")
+_lib.check(L.nngp_allgather_states(x.data_ptr(), y.data_ptr(), 6, torch.cuda.current_stream().cuda_stream))
+torch.cuda.synchronize(); assert torch.equal(x, y)
+assert L.nngp_comm_destroy() == 0
+print("deadline ok", flush=True)
+'''
+    root = os.path.dirname(HERE)
+    p = subprocess.run([sys.executable, '-c', code], env=dict(os.environ, NNGP_ROOT=root, NNGP_COMM_TIMEOUT_S='5'),
+                       capture_output=True, text=True, timeout=100)
+    print(p.stdout[-1500:])
+    assert p.returncode == 0 and 'deadline ok' in p.stdout, (p.stdout[-2000:], p.stderr[-3000:])

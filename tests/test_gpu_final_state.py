@@ -123,3 +123,28 @@ def test_fhn_pde_d800_n512_final_state_vs_serial_fine(gpu):
     e = np.max(np.abs(r['u'][rows, :, -1] - P['fine_rows']), axis=1)
     print('FHN-PDE d=800 N=512: K', r['k'], 'final-state error per sampled boundary', dict(zip(rows.tolist(), e)))
     assert r['converged'] and float(e.max()) <= 1e-6
+
+
+@pytest.mark.timeout(300)
+def test_hopf_n128_throughput_schedule_bitwise_oracle_loop_and_final_state(gpu):
+    """bench.py's own headline-config solve, `hopf_n128_to_convergence`: BASELINE configs[1] (Hopf
+    N = 128, RK1 16 / RK4 13 600 000 steps per slice -- Hopf.py's Nf x 10^4 schedule, unpaged;
+    nn = 15, n_restarts = 2, fatol = xatol = 0.1, seed 45; Hopf.py:65-84) to convergence (~40 s).
+    K, conv_int, the first three iterates and the SHA-256 of every iterate equal the CPU oracle
+    loop's (tests/golden/hopf128_13m_nngp.npz, gen_oracle_loops.py: K = 15, 560 s on 8 cores), and
+    the final state is within 1e-6 of the serial fine solution (128 x 13.6e6 RK4 steps one after
+    another; the oracle loop's own error is 3.6e-9)."""
+    P = golden('hopf128_13m_nngp.npz')
+    ode = gpu.Hopf(normalization='-11')
+    s = gpu.SolverRK(ode.get_vector_field(), Ng=16, Nf=2048 * 85 * 10000 // 128, F='RK4', G='RK1',
+                     thresh=float('inf'))
+    r = gpu.Parareal(ode, s, [-20, 500], 128, epsilon=5e-7, verbose=None).run(
+        model='nngp', nn=15, n_restarts=2, fatol=0.1, xatol=0.1, seed=45)
+    err = float(np.max(np.abs(r['u'][:, :, -1] - P['fine'])))
+    print(f"Hopf N=128 13.6e6: K={r['k']} (oracle loop {int(P['k'])}) conv_int {r['conv_int']} "
+          f"final-state error {err:.3e} (oracle loop {float(P['final_err']):.3e})")
+    assert r['converged'] and r['k'] == int(P['k']) == 15
+    assert r['conv_int'] == [int(c) for c in P['conv_int']]
+    assert np.array_equal(r['u'][:, :, :3], P['u3'])
+    assert _digest(r['u']) == str(P['digest'])
+    assert err <= 1e-6

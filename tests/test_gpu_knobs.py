@@ -48,13 +48,13 @@ KNOBS = [
     ('burgers', 'NNGP_SEL_PROF', '1'),
 ]
 # knobs whose neutrality needs a setting these runs do not have, tested where they apply:
-# NNGP_SHARD_EMULATE_RANKS (a one-rank RCCL communicator: test_gpu_distributed.py
-# ::test_native_rccl_comm_and_sharded_sweep_one_rank plays 3, 7 and 8 ranks against the unsharded run)
+# NNGP_COMM_TIMEOUT_S (the communicator's deadline: test_gpu_distributed.py
+# ::test_comm_init_without_peers_returns_in_bounded_time, a 2-rank init with no peer)
 # NNGP_KEY_LDS (selects over more than 4 096 rows: test_gpu_kernels.py
 # ::test_knn_streaming_select_vs_oracle runs every case with and without the LDS key cache)
 # NNGP_G_SIDE (an unsplit PDE sweep, i.e. without speculation: test_gpu_parareal.py
 # ::test_g_side_stream_is_bitwise)
-COVERED_ELSEWHERE = ['NNGP_SHARD_EMULATE_RANKS', 'NNGP_KEY_LDS', 'NNGP_G_SIDE']
+COVERED_ELSEWHERE = ['NNGP_COMM_TIMEOUT_S', 'NNGP_KEY_LDS', 'NNGP_G_SIDE']
 
 
 @pytest.mark.parametrize('case,knob,value', KNOBS)

@@ -66,24 +66,25 @@ def test_published_burgers59_gparareal_k_exact(gpu):
 
 
 @pytest.mark.timeout(300)
-def test_published_burgers59_nngp_straddle_over_seeds(gpu):
-    """Burgers.py T = 5.9 nnGParareal (nn = 18; published K = 14, seed 45).  Here the error maxima
-    decay slowly through iterations 11-16 (a plateau of 5e-7 .. 1e-6 around epsilon = 5e-7), and
-    at the published run's last iteration, 14, EVERY seed 45-50 sits just above epsilon (1.03 to
-    1.6 epsilon: 5.13e-7 for seed 45), so they need one to three more iterations: K = 15, 16, 15, 16,
-    17, 15.  The published run's iteration-14 maximum fell just below epsilon -- a threshold
-    straddle on a plateau, which the last-ulp differences of the GP arithmetic (XLA / OpenBLAS
-    against the restatement) decide.  (The published 200-page schedule: K = 16,
-    6.85e-7 at iteration 14; test_published_burgers59_nngp_paged.)"""
+def test_published_burgers59_nngp_k_band_over_seeds(gpu):
+    """Burgers.py T = 5.9 nnGParareal (nn = 18; published K = 14, seed 45).  PARITY UNPINNED at the
+    level of K: the reference's per-iteration errors for this run sit in a pickle the safe loaders
+    refuse, so nothing pins which side of epsilon its iteration 14 fell on beyond
+    the published K.  Here the error maxima decay slowly through iterations 11-16 (a plateau of
+    5e-7 .. 1e-6 around epsilon = 5e-7) and seeds 45-50 have given K = 15, 16, 15, 16, 17, 15 --
+    all on the same side, which a systematic last-ulp offset of the GP arithmetic (XLA / OpenBLAS
+    against the restatement) could explain as well as chance.  Asserted: every
+    seed converges within a band around the published K, 14 <= K <= 17, and the iteration-14
+    error maxima are printed (the paged schedule: test_published_burgers59_nngp_paged)."""
     ks, e14 = {}, {}
     for seed in (45, 46, 47, 48, 49, 50):
         o, pk = _run(gpu, 'burgers59_128_nngp', seed=seed)
         assert o['converged'] and pk == 14
-        ks[seed], e14[seed] = o['K'], o['err_max'][13]
-    print('Burgers T=5.9 nnGP K over seeds:', ks, 'iteration-14 error maxima:', e14)
-    assert ks[45] == 15 and EPS < e14[45] < 1.1 * EPS
-    assert all(15 <= k <= 17 for k in ks.values())
-    assert all(EPS < e < 1.6 * EPS for e in e14.values())
+        ks[seed] = o['K']
+        e14[seed] = o['err_max'][13] if len(o['err_max']) > 13 else float('nan')
+    print('Burgers T=5.9 nnGP K over seeds:', ks, '(published 14); iteration-14 error maxima / epsilon:',
+          {s_: round(e / EPS, 3) for s_, e in e14.items()})
+    assert all(14 <= k <= 17 for k in ks.values())
 
 
 # --------------------------------------------------------------------------------- long (opt-in)
