@@ -280,9 +280,11 @@ def published_k_table(torch, g, live_extra=None):
     return {'rows': rows, 'parareal_exact': cnt(det), 'exact_live': cnt(live), 'exact_recorded': cnt(rec),
             'note': 'name = <system>_<N>_<model>[_paged]; unpaged = Nf/N RK steps per slice; paged = the '
                     'published scripts\' RK_thresh schedule (every one of 25 / 200 pages re-uses all Nf/N '
-                    'steps: a 25x / 200x finer fine step). The two fine solutions differ by more than '
-                    'roundoff for the stiff / long runs (tools/paging_delta.py), and nnGParareal K can '
-                    'move with the schedule (FHN-PDE d_x = 10: 11 paged, 9 unpaged; d_x = 12: 10 / 8), so '
+                    'steps: a 25x / 200x finer fine step). FHN-PDE d_x = 10 / 12 get 26 pages (float page '
+                    'arithmetic), so their paged F integrates 4 % past every slice end and differs from the '
+                    'unpaged F by 1e4 epsilon; where the pages cover the slice (d_x = 16) the two differ by '
+                    '1e-13 (profiles/r06/paging_delta.txt). nnGParareal K moves with the schedule (FHN-PDE '
+                    'd_x = 10: 11 paged, 9 unpaged; d_x = 12: 10 / 8), so '
                     'each row states its schedule; nnGP mismatches are discussed in DESIGN.md 5'}
 
 

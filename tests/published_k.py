@@ -13,16 +13,24 @@ Each entry reproduces one script's settings (file:line cited in its builder):
                          u0 = 0.5(cos(4.5 pi x)+1) through '-11' with bounds [0, 1]; nnGP nn=18.
 
 Paging.  Every script sets RK_thresh = Nf/N/scaling (25, or 200 for Burgers), so the published
-runs integrate each slice `scaling` times over with the full per-slice point count on 1/scaling of
-the slice (RK_last's quirk, new_lib.py:57-69).  That is the same ODE integrated
-with a scaling-times finer step: RK8 at Nf/N >= 40 000 steps per slice is at roundoff already,
-so paging changes the fine solution only in its roundoff.  `paged=False` (RK_thresh = inf) runs the
-Nf/N-step schedule instead, 25-200x cheaper; `paged=True` reproduces the published work exactly.
-Which one each pinned result used is recorded with it (tests/test_gpu_published_k.py).
+runs integrate each slice page by page, every page with the full per-slice step count (RK_last's
+quirk, new_lib.py:57-69): a `scaling`-times finer step, 25-200x the work.  The
+paged fine solution is NOT the unpaged one to roundoff (tools/paging_delta.py):
+  * the page list is computed in floating point: FHN-PDE d_x = 10 / 12 get 26 pages of
+    Nf/N/25 = 7812.6 / 7812.96 points, so F integrates 4 % PAST every slice end (d_x = 16, Hopf,
+    Burgers: 25 / 200 pages covering the slice; TomLab: 109 pages + a remainder page);
+  * so d_x = 10 / 12 paged F is 6.1e-3 / 8.4e-3 (1.2e4 / 1.7e4 epsilon) from unpaged F on slice 0,
+    while d_x = 16 paged (25 pages) is 1.3e-13 from unpaged: the finer step alone is roundoff
+    (profiles/r06/paging_delta.txt);
+  * nnGParareal K moves with the schedule: FHN-PDE d_x = 10 gives 11 paged / 9 unpaged, d_x = 12
+    10 / 8 (profiles/r05/published_k/).
+`paged=False` (RK_thresh = inf) runs the Nf/N-step schedule, 25-200x cheaper; `paged=True`
+reproduces the published work exactly.  Every recorded row states its schedule
+(name suffix `_paged`; tests/test_gpu_published_k.py, bench.py published_k).
 
-The GP (full-data GParareal) entries of FHN-PDE d_x = 10 / 12 are not built: at N = 512 each
-training round factors 9*d = 1 800 / 2 592 dense matrices of ~4 000 rows (~240 GB of scratch and
-~4e13 flops per Nelder-Mead round, up to 400 rounds per iteration).
+The GP (full-data GParareal) entries of FHN-PDE d_x = 10 / 12 factor 9*d = 1 800 / 2 592 dense
+matrices of up to ~4 100 rows per Nelder-Mead round (~240 GB, run in slabs of NNGP_GPF_SLAB_GB;
+~4e13 flops per round, up to 400 rounds per iteration).
 """
 import math
 
