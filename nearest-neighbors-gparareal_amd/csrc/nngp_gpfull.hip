@@ -379,6 +379,214 @@ __global__ void __launch_bounds__(256, 3) gpf_update_kernel(double *__restrict__
         gpf_update_tile<false>(Ab, ld, n, p0, pb, i0, j0, ti == tj, Li, Lj);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Left-looking order on 64-column panels (round 6, the default; NNGP_GPF_ORDER=1 keeps the
+// right-looking 32-column order above).  Per panel c0 (width pb = min(64, n - c0)):
+//   gpf_ll_gemm_kernel  A[c0..n][c0..c0+pb) -= L[c0..n][0..c0) L[c0..c0+pb)[0..c0)^T: one 64-row
+//                       tile per workgroup, the whole k = 0..c0 sum accumulated on the FP64 matrix
+//                       cores and subtracted once (OpenBLAS's potrf also subtracts a K-block's
+//                       register-accumulated product at once).  Row n = y^T rides along: its
+//                       update is the forward solve's z_j -= sum_k z_k L_jk.
+//   gpf_ll_diag_kernel  one wave factors the 64x64 diagonal block (lane i = row i), L11 and 1/L_jj
+//                       into Lpan (column-major, so the lanes' stores coalesce)
+//   gpf_ll_rows_kernel  the rows below: x L11^T = a by substitution, one lane per row, 256 rows per
+//                       workgroup sharing one LDS copy of L11; its first workgroup also writes L11
+//                       into A
+// Why: the right-looking 32-column update re-reads and re-writes the whole trailing matrix per
+// panel (4 flop/B, HBM-bound at ~52 % of HBM); the left-looking panel GEMM reads
+// each L row once per panel and writes only the panel (nb/4 = 16 flop/B), and the chain per
+// Nelder-Mead round has 3 launches per 64 columns instead of per 32.
+static constexpr int LB = 64;                // panel width
+static constexpr int LPS64 = LB * LB + LB;   // Lpan doubles per matrix: L11 column-major | 1/L_jj
+static constexpr int LKC = 32;               // k chunk of the panel GEMM
+static constexpr int LKS = LKC + 2;          // its LDS row stride (the gpf_update_tile operand pattern)
+
+// (matrix, tile) of linear workgroup `lin`: workgroups go round-robin over the 8 XCDs, the k-th of
+// XCD x takes matrix x + 8 (k / T), tile k % T -- a matrix's tiles share one L2 (grid y padded to 8)
+__device__ __forceinline__ void gpf_xcd_map(int lin, int T, int &b, int &t) {
+    const int kx = lin >> 3;
+    b = (lin & 7) + 8 * (kx / T);
+    t = kx % T;
+}
+
+template <bool FULL>   // FULL: the tile's 64 rows exist and pb == LB -- no guards
+__device__ __forceinline__ void gpf_ll_gemm_tile(double *__restrict__ Ab, int ld, int n, int c0, int pb, int r0,
+                                                 bool diag, double *Sa, double *Sb) {
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int kq = lane >> 4, cl = lane & 15;
+    const int sr = tid >> 5, sk = tid & 31;   // staging: rows sr + 8u, column sk of the chunk
+    double *SB = diag ? Sa : Sb;              // the diagonal tile's B rows are its own A rows
+    double va[8], vb[8];
+#define GPF_LL_LOAD(kk)                                                                                  \
+    _Pragma("unroll") for (int u = 0; u < 8; u++) {                                                    \
+        const int rr = sr + 8 * u;                                                                     \
+        va[u] = (FULL || r0 + rr <= n) ? Ab[(size_t)(r0 + rr) * ld + (kk) + sk] : 0.0;                 \
+        vb[u] = (!diag && (FULL || rr < pb)) ? Ab[(size_t)(c0 + rr) * ld + (kk) + sk] : 0.0;           \
+    }
+    f64x4 acc[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; cb++) acc[cb] = f64x4{0.0, 0.0, 0.0, 0.0};
+    const int ncb = diag ? w + 1 : 4;         // the diagonal tile: column blocks at or left of the wave's rows
+    GPF_LL_LOAD(0)
+    for (int kk = 0; kk < c0; kk += LKC) {
+        __syncthreads();                      // the previous chunk's operand reads are done
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            Sa[(sr + 8 * u) * LKS + sk] = va[u];
+            if (!diag) Sb[(sr + 8 * u) * LKS + sk] = vb[u];
+        }
+        __syncthreads();
+        if (kk + LKC < c0) {                  // the next chunk's loads fly under this chunk's MFMAs
+            GPF_LL_LOAD(kk + LKC)
+        }
+#pragma unroll
+        for (int k = 0; k < LKC; k += 4) {
+            const double av = Sa[(16 * w + cl) * LKS + k + kq];
+#pragma unroll
+            for (int cb = 0; cb < 4; cb++)
+                if (cb < ncb)
+                    acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, SB[(16 * cb + cl) * LKS + k + kq], acc[cb], 0,
+                                                                   0, 0);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int i = 16 * w + kq + 4 * r;
+#pragma unroll
+        for (int cb = 0; cb < 4; cb++) {
+            const int j = 16 * cb + cl;
+            if (cb < ncb && (FULL || (r0 + i <= n && j < pb)) && (!diag || j <= i)) {
+                double *p = Ab + (size_t)(r0 + i) * ld + c0 + j;
+                *p = *p - acc[cb][r];
+            }
+        }
+    }
+#undef GPF_LL_LOAD
+}
+
+__global__ void __launch_bounds__(256, 2) gpf_ll_gemm_kernel(double *__restrict__ A, int n, int c0, int pb,
+                                                              const int32_t *__restrict__ fail, int T, int nmat) {
+    int b, t;
+    gpf_xcd_map(blockIdx.x + blockIdx.y * T, T, b, t);
+    if (b >= nmat || fail[b]) return;
+    const int ld = n + 1;
+    double *Ab = A + (size_t)b * ld * ld;
+    const int r0 = c0 + LB * t;
+    __shared__ double Sa[LB * LKS], Sb[LB * LKS];
+    if (r0 + LB - 1 <= n && pb == LB)
+        gpf_ll_gemm_tile<true>(Ab, ld, n, c0, pb, r0, t == 0, Sa, Sb);
+    else
+        gpf_ll_gemm_tile<false>(Ab, ld, n, c0, pb, r0, t == 0, Sa, Sb);
+}
+
+template <bool FMA>
+__device__ __forceinline__ double gpf_msub(double x, double a, double b) {   // x - a*b
+    if constexpr (FMA) return fma(-a, b, x);
+    else return x - a * b;
+}
+
+// The 64x64 diagonal block of one matrix per wave (lane i = row i, right-looking by columns:
+// L_jj = sqrt(a_jj), L_ij = a_ij * (1/L_jj), a_ik -= L_ij L_kj for k > j), the column broadcast
+// through LDS.  Lanes i < k carry garbage in a[k] (the upper triangle), never stored.
+template <bool FMA>
+__global__ void __launch_bounds__(64) gpf_ll_diag_kernel(const double *__restrict__ A, int n, int c0, int pb,
+                                                          int32_t *__restrict__ fail, double *__restrict__ Lpan,
+                                                          int nmat) {
+    const int b = blockIdx.x;
+    if (b >= nmat || fail[b]) return;
+    const int i = threadIdx.x, ld = n + 1;
+    const double *Ab = A + (size_t)b * ld * ld;
+    __shared__ __attribute__((aligned(16))) double col[LB];
+    double a[LB];
+#pragma unroll
+    for (int k = 0; k < LB; k++) a[k] = (i < pb && k <= i) ? Ab[(size_t)(c0 + i) * ld + c0 + k] : 0.0;
+    bool bad = false;
+    double myr = 1.0;
+#pragma unroll
+    for (int j = 0; j < LB; j++) {
+        if (j < pb) {
+            const double djj = lane_double(a[j], j);
+            bad = bad || !(djj > 0.0);
+            const double ljj = sqrt(djj);
+            const double rj = 1.0 / ljj;
+            const double lij = a[j] * rj;
+            a[j] = (i == j) ? ljj : lij;
+            myr = (i == j) ? rj : myr;
+            col[i] = a[j];
+            wave_sync_lds();
+#pragma unroll
+            for (int k = j + 1; k < LB; k++) a[k] = gpf_msub<FMA>(a[k], a[j], col[k]);
+            wave_sync_lds();
+        }
+    }
+    if (bad) {
+        if (i == 0) fail[b] = 1;
+        return;
+    }
+    double *Lb = Lpan + (size_t)b * LPS64;
+#pragma unroll
+    for (int k = 0; k < LB; k++) Lb[k * LB + i] = (i < pb && k <= i) ? a[k] : 0.0;
+    Lb[LB * LB + i] = myr;
+}
+
+template <bool FMA>
+__global__ void __launch_bounds__(256) gpf_ll_rows_kernel(double *__restrict__ A, int n, int c0, int pb,
+                                                           const int32_t *__restrict__ fail,
+                                                           const double *__restrict__ Lpan, int T, int nmat) {
+    int b, t;
+    gpf_xcd_map(blockIdx.x + blockIdx.y * T, T, b, t);
+    if (b >= nmat || fail[b]) return;
+    const int ld = n + 1;
+    double *Ab = A + (size_t)b * ld * ld;
+    __shared__ __attribute__((aligned(16))) double L[LPS64];   // column-major L11 | 1/L_jj
+    __shared__ double X[4][LB * 17];                           // per wave: 64 rows x 16 columns
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const double *Lsrc = Lpan + (size_t)b * LPS64;
+    for (int e = tid; e < LPS64; e += 256) L[e] = Lsrc[e];
+    __syncthreads();
+    if (t == 0)   // L11 into A's diagonal block, coalesced along the rows
+        for (int e = tid; e < LB * LB; e += 256) {
+            const int ii = e >> 6, k = e & 63;
+            if (k <= ii && ii < pb) Ab[(size_t)(c0 + ii) * ld + c0 + k] = L[k * LB + ii];
+        }
+    const int rw = c0 + pb + 256 * t + 64 * w;   // this wave's first row
+    if (rw > n) return;                          // (no barrier follows)
+    double *Xw = X[w];
+    double x[LB];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {   // stage 16 columns of the wave's 64 rows, coalesced
+#pragma unroll
+        for (int v = 0; v < 16; v++) {
+            const int e = lane + 64 * v, rr = e >> 4, k = 16 * q + (e & 15);
+            Xw[rr * 17 + (e & 15)] = (rw + rr <= n && k < pb) ? Ab[(size_t)(rw + rr) * ld + c0 + k] : 0.0;
+        }
+        wave_sync_lds();
+#pragma unroll
+        for (int c = 0; c < 16; c++) x[16 * q + c] = Xw[lane * 17 + c];
+        wave_sync_lds();
+    }
+#pragma unroll
+    for (int j = 0; j < LB; j++) {
+        if (j < pb) {
+            x[j] = x[j] * L[LB * LB + j];
+#pragma unroll
+            for (int k = j + 1; k < LB; k++) x[k] = gpf_msub<FMA>(x[k], x[j], L[j * LB + k]);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+#pragma unroll
+        for (int c = 0; c < 16; c++) Xw[lane * 17 + c] = x[16 * q + c];
+        wave_sync_lds();
+#pragma unroll
+        for (int v = 0; v < 16; v++) {
+            const int e = lane + 64 * v, rr = e >> 4, k = 16 * q + (e & 15);
+            if (rw + rr <= n && k < pb) Ab[(size_t)(rw + rr) * ld + c0 + k] = Xw[rr * 17 + (e & 15)];
+        }
+        wave_sync_lds();
+    }
+}
+
 __device__ __forceinline__ double block_sum(double v, double *red) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -497,25 +705,51 @@ int gpfull_mean(const double *X, int64_t rows, int d, const double *q, const dou
 }
 
 // The batched -LML pipeline for nb points (device pts), D2 [n][n] given; A: nb*(n+1)^2 scratch.
+// Factor order: NNGP_GPF_ORDER=0 (default) the left-looking 64-column panels, 1 the right-looking
+// 32-column order (rounds 3-5); NNGP_GPF_FMA=1 fuses the diagonal factor's and the row solve's
+// updates (left-looking order only).
 static int gpf_eval(const double *D2, int n, const double *Y, int d, const GPPoint *pts, int nb, double *A,
                     int32_t *fail, double *fval, double *alpha_out, double *Lpan, hipStream_t st) {
     NNGP_HIP_CHECK(hipMemsetAsync(fail, 0, sizeof(int32_t) * nb, st));
     const unsigned bx = (unsigned)((n + GPF_BROWS - 1) / GPF_BROWS + 1);   // + the y row's block
     hipLaunchKernelGGL(gpf_build_kernel, dim3(bx, nb), dim3(256), 0, st, D2, n, Y, d, pts, A, fail);
     NNGP_LAUNCH_CHECK();
-    for (int p0 = 0; p0 < n; p0 += GPB) {
-        const int pb = std::min(GPB, n - p0);
-        const int below = n + 1 - p0 - pb;   // includes row n (y)
-        const unsigned chunks = (unsigned)std::max(1, (below + 63) / 64);
-        hipLaunchKernelGGL(gpf_diag_kernel, dim3((nb + 1) / 2), dim3(64), 0, st, A, n, p0, pb, nb, fail, Lpan);
-        if (pb == GPB)
-            hipLaunchKernelGGL(gpf_rows_kernel<true>, dim3(chunks, nb), dim3(64), 0, st, A, n, p0, pb, fail, Lpan);
-        else
-            hipLaunchKernelGGL(gpf_rows_kernel<false>, dim3(chunks, nb), dim3(64), 0, st, A, n, p0, pb, fail, Lpan);
-        const int nt = (below + GPF_TM - 1) / GPF_TM;
-        const int ntiles = nt * (nt + 1) / 2;
-        const dim3 grid((unsigned)(ntiles + 1), (unsigned)((nb + 7) / 8 * 8));   // y padded: XCD order
-        hipLaunchKernelGGL(gpf_update_kernel, grid, dim3(256), 0, st, A, n, p0, pb, fail, Lpan, ntiles, nb);
+    const unsigned ny8 = (unsigned)((nb + 7) / 8 * 8);   // grid y padded: XCD order
+    if (env_int("NNGP_GPF_ORDER", 0) == 0) {
+        const bool fma = env_int("NNGP_GPF_FMA", 0) != 0;
+        for (int c0 = 0; c0 < n; c0 += LB) {
+            const int pb = std::min(LB, n - c0);
+            if (c0 > 0) {
+                const int T = (n + 1 - c0 + LB - 1) / LB;
+                hipLaunchKernelGGL(gpf_ll_gemm_kernel, dim3(T, ny8), dim3(256), 0, st, A, n, c0, pb, fail, T, nb);
+            }
+            if (fma)
+                hipLaunchKernelGGL(gpf_ll_diag_kernel<true>, dim3(nb), dim3(64), 0, st, A, n, c0, pb, fail, Lpan, nb);
+            else
+                hipLaunchKernelGGL(gpf_ll_diag_kernel<false>, dim3(nb), dim3(64), 0, st, A, n, c0, pb, fail, Lpan, nb);
+            const int TR = (n + 1 - c0 - pb + 255) / 256;   // >= 1: row n is always below
+            if (fma)
+                hipLaunchKernelGGL(gpf_ll_rows_kernel<true>, dim3(TR, ny8), dim3(256), 0, st, A, n, c0, pb, fail, Lpan,
+                                   TR, nb);
+            else
+                hipLaunchKernelGGL(gpf_ll_rows_kernel<false>, dim3(TR, ny8), dim3(256), 0, st, A, n, c0, pb, fail,
+                                   Lpan, TR, nb);
+        }
+    } else {
+        for (int p0 = 0; p0 < n; p0 += GPB) {
+            const int pb = std::min(GPB, n - p0);
+            const int below = n + 1 - p0 - pb;   // includes row n (y)
+            const unsigned chunks = (unsigned)std::max(1, (below + 63) / 64);
+            hipLaunchKernelGGL(gpf_diag_kernel, dim3((nb + 1) / 2), dim3(64), 0, st, A, n, p0, pb, nb, fail, Lpan);
+            if (pb == GPB)
+                hipLaunchKernelGGL(gpf_rows_kernel<true>, dim3(chunks, nb), dim3(64), 0, st, A, n, p0, pb, fail, Lpan);
+            else
+                hipLaunchKernelGGL(gpf_rows_kernel<false>, dim3(chunks, nb), dim3(64), 0, st, A, n, p0, pb, fail, Lpan);
+            const int nt = (below + GPF_TM - 1) / GPF_TM;
+            const int ntiles = nt * (nt + 1) / 2;
+            const dim3 grid((unsigned)(ntiles + 1), ny8);
+            hipLaunchKernelGGL(gpf_update_kernel, grid, dim3(256), 0, st, A, n, p0, pb, fail, Lpan, ntiles, nb);
+        }
     }
     NNGP_LAUNCH_CHECK();
     hipLaunchKernelGGL(gpf_lml_kernel, dim3(nb), dim3(256), 0, st, A, n, fail, fval);
@@ -547,7 +781,7 @@ struct GPFWork {   // device buffers of one call
 static int gpf_workspace(int n, int nb, GPFWork &w) {
     int err = 0;
     const size_t nn = (size_t)n * n, mm = (size_t)(n + 1) * (n + 1);
-    const size_t bytes = sizeof(double) * (nn + (size_t)nb * mm + nb + (size_t)nb * LPS) + sizeof(GPPoint) * nb +
+    const size_t bytes = sizeof(double) * (nn + (size_t)nb * mm + nb + (size_t)nb * LPS64) + sizeof(GPPoint) * nb +
                          sizeof(int32_t) * nb + 64;
     char *p = (char *)workspace(bytes, &err, 3);
     if (err) return err;
@@ -555,7 +789,7 @@ static int gpf_workspace(int n, int nb, GPFWork &w) {
     w.A = w.D2 + nn;
     w.fval = w.A + (size_t)nb * mm;
     w.Lpan = w.fval + nb;
-    w.pts = (GPPoint *)(w.Lpan + (size_t)nb * LPS);
+    w.pts = (GPPoint *)(w.Lpan + (size_t)nb * LPS64);
     w.fail = (int32_t *)(w.pts + nb);
     return NNGP_OK;
 }
@@ -566,10 +800,13 @@ static int gpf_check(int64_t rows, int d, int n_fit) {
     return NNGP_OK;
 }
 
-// points per batch: all fits, capped so the factor scratch stays under ~8 GB
+// points per batch: all fits, capped so the factor slab stays under NNGP_GPF_SLAB_MB (default 32 GB
+// of the 288 GB HBM: FHN-PDE d_x = 10 at N = 512 factors 1 800 matrices of ~4 100 rows per round,
+// 240 GB in one slab, so its rounds run in chunks of ~230 matrices, each chunk filling the chip)
 static int gpf_batch_cap(int n, int n_fit) {
     const size_t per = sizeof(double) * (size_t)(n + 1) * (n + 1);
-    const size_t cap = std::max<size_t>(1, ((size_t)8 << 30) / per);
+    const size_t slab = (size_t)std::max(1, env_int("NNGP_GPF_SLAB_MB", 32768)) << 20;
+    const size_t cap = std::max<size_t>(1, slab / per);
     return (int)std::min<size_t>(cap, (size_t)n_fit);
 }
 

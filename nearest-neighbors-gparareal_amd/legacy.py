@@ -112,10 +112,7 @@ class Parareal(_Parareal):
         self.ode_name = ode_name
         self.n = self.u0.shape[0]
 
-    def run(self, *args, **kwargs):
-        # new_lib's _parareal reads self.Ng / self.Nf / self.F / self.G / self.RK_thresh when it
-        # runs (new_lib.py:902-997), and the scalability scripts re-assign them after construction
-        # (Hopf.py:68-69: s.Nf = s.Nf * 10000; s.RK_thresh = s.Nf/s.N/scaling)
+    def _setup_solver(self):
         s, N = self.solver, self.N
         Ng, Nf = int(self.Ng), int(self.Nf)
         if (Ng % N != 0) or (Nf % Ng != 0):
@@ -125,6 +122,16 @@ class Parareal(_Parareal):
         s.Ng, s.Nf, s.Ng_total, s.Nf_total = Ng // N, Nf // N, Ng, Nf
         s.F, s.G = self.F, self.G
         s.RK_thresh = self.RK_thresh
+
+    def load_int_dump(self, *args, **kwargs):
+        self._setup_solver()
+        return super().load_int_dump(*args, **kwargs)
+
+    def run(self, *args, **kwargs):
+        # new_lib's _parareal reads self.Ng / self.Nf / self.F / self.G / self.RK_thresh when it
+        # runs (new_lib.py:902-997), and the scalability scripts re-assign them after construction
+        # (Hopf.py:68-69: s.Nf = s.Nf * 10000; s.RK_thresh = s.Nf/s.N/scaling)
+        self._setup_solver()
         return super().run(*args, **kwargs)
 
 

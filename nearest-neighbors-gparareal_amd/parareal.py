@@ -817,6 +817,12 @@ class Parareal():
                 if verbose == 'v':
                     print('Early stopping due to user condition.')
                 break
+            # not in the reference: a wall-clock deadline (time.time() value) for runs longer than
+            # one session, resumed later from their store_int dump (tools/published_k_run.py)
+            if kwargs.get('stop_at') is not None and time.time() > kwargs['stop_at']:
+                if verbose == 'v':
+                    print('Stopping at the stop_at deadline; resume from the store_int dump.')
+                break
 
         timings = {'F_time': F_time, 'G_time': G_time, 'F_time_serial_avg': F_time_serial,
                    'spec_hits': list(self.spec_hits)}

@@ -11,6 +11,10 @@ Each entry reproduces one script's settings (file:line cited in its builder):
                          u0 = seed-45 rand(d) through '-11' with bounds +-1; nnGP nn=20.
   * Burgers.py:27-122 -- T = 5.9, N = d = 128, Ng = 4N RK1, Nf = Ng*10^4 RK8, eps 5e-7,
                          u0 = 0.5(cos(4.5 pi x)+1) through '-11' with bounds [0, 1]; nnGP nn=18.
+  * TomLab.py:66-122  -- ThomasLabyrinth through '-11' with bounds +-12, T = 10 / 100 / 100 for
+                         N = 32 / 256 / 512, Ng = 10N RK1, Nf = Ng*ceil(1e9/Ng) RK4, eps 5e-7;
+                         nnGP nn=18, n_restarts=1, fatol=xatol=1e-3, seed 45; GP fatol=xatol=0.1.
+                         Chaotic: Parareal K is asserted exactly, nnGP K against a seed spread.
 
 Paging.  Every script sets RK_thresh = Nf/N/scaling (25, or 200 for Burgers), so the published
 runs integrate each slice page by page, every page with the full per-slice step count (RK_last's
@@ -44,6 +48,9 @@ PUBLISHED_K = {
     ('fhn16', 512, 'para'): 79, ('fhn16', 512, 'nngp'): 6,
     ('burgers59', 128, 'para'): 90, ('burgers59', 128, 'gp'): 8, ('burgers59', 128, 'nngp'): 14,
     ('burgers5', 128, 'para'): 10, ('burgers5', 128, 'gp'): 6, ('burgers5', 128, 'nngp'): 9,
+    ('tomlab', 32, 'para'): 30, ('tomlab', 32, 'gp'): 25, ('tomlab', 32, 'nngp'): 24,
+    ('tomlab', 256, 'para'): 256, ('tomlab', 256, 'nngp'): 159,     # TomLab GP N=256/512 did not finish in 48 h
+    ('tomlab', 512, 'para'): 180, ('tomlab', 512, 'nngp'): 69,
 }
 
 # run() keyword arguments of each script's model branch
@@ -52,7 +59,10 @@ RUN_KW = {
              'nngp': dict(model='nngp', fatol=1e-1, xatol=1e-1, nn=15, n_restarts=2, seed=45)},   # Hopf.py:77-84
     'fhn': {'para': {}, 'gp': dict(model='gpjax'), 'nngp': dict(model='nngp', nn=20)},           # FHN_PDE.py:169-175
     'burgers': {'para': {}, 'gp': dict(model='gpjax'), 'nngp': dict(model='nngp', nn=18)},       # Burgers.py:116-122
+    'tomlab': {'para': {}, 'gp': dict(model='gpjax', fatol=1e-1, xatol=1e-1),                     # TomLab.py:110-119
+               'nngp': dict(model='nngp', nn=18, n_restarts=1, fatol=1e-3, xatol=1e-3, seed=45)},
 }
+TOMLAB_T = {32: 10, 64: 10, 128: 40, 256: 100, 512: 100}   # TomLab.py:72-82
 
 FHN_SETTINGS = {10: (3, 150, 'RK2'), 12: (12, 550, 'RK2'), 14: (25, 950, 'RK2'), 16: (25, 1100, 'RK4')}  # FHN_PDE.py:34-51
 
@@ -86,6 +96,18 @@ def burgers(gpu, T=5.9, N=128, paged=False, verbose=None):
     return s
 
 
+def tomlab(gpu, N, paged=False, verbose=None):
+    """TomLab.py:66-101 (ThomasLabyrinth_n: '-11' with bounds +-12; u0 = Systems._tr(u0); 109
+    pages + a remainder page when paged)."""
+    ode = gpu.ThomasLabyrinth(normalization='-11')
+    Ng = N * 10
+    Nf = Ng * int(math.ceil(1e9 / Ng))
+    s = gpu.legacy.Parareal(f=ode.get_vector_field(), tspan=[0, TOMLAB_T[N]], u0=ode.get_init_cond(), N=N, Ng=Ng,
+                            Nf=Nf, epsilon=5e-7, F='RK4', G='RK1', ode_name='TomLab', verbose=verbose)
+    s.RK_thresh = s.Nf / s.N / 109 if paged else float('inf')
+    return s
+
+
 def build(gpu, name, verbose=None):
     """name = '<system>_<N>_<model>[_paged]', e.g. 'hopf_128_nngp', 'fhn10_512_para',
     'burgers59_128_nngp_paged'.  Returns (Parareal, run kwargs, published K)."""
@@ -99,6 +121,8 @@ def build(gpu, name, verbose=None):
     elif system.startswith('burgers'):
         T = {'burgers59': 5.9, 'burgers5': 5}[system]
         s, kw = burgers(gpu, T, N, paged, verbose), RUN_KW['burgers'][model]
+    elif system == 'tomlab':
+        s, kw = tomlab(gpu, N, paged, verbose), RUN_KW['tomlab'][model]
     else:
         raise ValueError(name)
     return s, dict(kw), PUBLISHED_K.get((system, N, model))

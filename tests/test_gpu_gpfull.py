@@ -63,10 +63,19 @@ def test_gpfull_lml_matches_reference_values(gpu):
         assert _close(a, b, _tol(x, th, jit)), (a, b, th, jit)
 
 
-@pytest.mark.parametrize('n', [1, 5, 31, 32, 33, 64, 100, 257, 600])
-def test_gpfull_lml_and_weights_vs_oracle(gpu, n):
-    """Panel edges (31/32/33), several panels, and a 600-row set (the size GParareal reaches)."""
+ORDERS = {'ll64': {'NNGP_GPF_ORDER': '0', 'NNGP_GPF_FMA': '0'}, 'll64_fma': {'NNGP_GPF_ORDER': '0', 'NNGP_GPF_FMA': '1'},
+          'rl32': {'NNGP_GPF_ORDER': '1', 'NNGP_GPF_FMA': '0'}}
+
+
+@pytest.mark.parametrize('order', sorted(ORDERS))
+@pytest.mark.parametrize('n', [1, 5, 31, 32, 33, 63, 64, 65, 100, 129, 257, 600])
+def test_gpfull_lml_and_weights_vs_oracle(gpu, n, order, monkeypatch):
+    """Panel edges (31/32/33 and 63/64/65), several panels, and a 600-row set (the size GParareal
+    reaches), in every factor order (NNGP_GPF_ORDER / NNGP_GPF_FMA; each against the oracle, as
+    they round differently); and a one-matrix slab (NNGP_GPF_SLAB_MB) bitwise the whole batch."""
     import torch
+    for k, v in ORDERS[order].items():
+        monkeypatch.setenv(k, v)
     rng = np.random.default_rng(n)
     x = rng.uniform(-1, 1, (n, 3))
     y = np.sin(2 * x) + 0.01 * rng.standard_normal((n, 3))
@@ -74,6 +83,9 @@ def test_gpfull_lml_and_weights_vs_oracle(gpu, n):
     jit = [-12.0, -14.0, -11.0, -16.0]
     coords = [0, 1, 2, 0]
     fv, al = _lml(gpu, torch, x, y, coords, jit, thetas, alpha=True)
+    monkeypatch.setenv('NNGP_GPF_SLAB_MB', str(max(1, 8 * (n + 1) ** 2 >> 20)))   # one matrix per chunk
+    fv1, al1 = _lml(gpu, torch, x, y, coords, jit, thetas, alpha=True)
+    assert np.array_equal(fv1, fv) and np.array_equal(np.nan_to_num(al1[:3]), np.nan_to_num(al[:3]))
     # sigma_x = 0: NaN kernel -> failed Cholesky -> +inf (the reference would raise from
     # solve_triangular's finite check here, so there is no reference value to compare with)
     assert np.isinf(fv[3]) and fv[3] > 0

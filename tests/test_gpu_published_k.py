@@ -1,8 +1,8 @@
 """The reference's published K table (VERDICT.md round 4 "Next round" 1)
 run at the published configurations on the legacy new_lib driver surface (nngp_amd.legacy) --
 tests/published_k.py builds each one from its script (Hopf.py, FHN_PDE.py, Burgers.py), file:line
-cited there, including why an unpaged F is the same integration as the scripts' paged one up to
-roundoff.
+cited there, including how the scripts' paged F differs from the unpaged one (SURVEY.md §0.4,
+tools/paging_delta.py): every row names its schedule.
 
 Every deterministic classic-Parareal K is asserted EXACTLY equal to the published one.  nnGParareal
 K follows fits that Nelder-Mead steers from the last bits of the GP arithmetic (SURVEY.md §0.6-0.7:

@@ -5,7 +5,15 @@ gpurun_out/published_k/ (copied to profiles/r05/ afterwards).
     python -u tools/published_k_run.py fhn10_512_para fhn10_512_nngp hopf_512_nngp ...
     python -u tools/published_k_run.py burgers59_128_nngp@46 ...     (another RNG seed; file name@46.json)
 
-Progress goes to stdout every iteration (verbose driver), so a long entry is never silent."""
+Progress goes to stdout every iteration (verbose driver), so a long entry is never silent.
+
+Runs longer than one GPU session (the full-data GParareal rows at published scale): with
+NNGP_PK_CKPT=<dir> every iteration's store_int dump goes to <dir>/<name>/ and a run that finds a
+dump there resumes from the newest one (bitwise the uninterrupted run, RNG stream included,
+tests/test_gpu_gpfull.py); NNGP_PK_BUDGET_S=<s> stops it after the first iteration that ends past
+<s> seconds and writes <name>.partial.json instead of <name>.json.  The dumps must be copied from
+gpurun_out/ back into <dir> (which travels to the box) between sessions."""
+import glob
 import json
 import os
 import sys
@@ -31,11 +39,29 @@ def main(names):
         print(f'=== {name}: published K {pk}; run kwargs {kw}; Nf/N {s.Nf // s.N}, RK_thresh {s.RK_thresh}',
               flush=True)
         t0 = time.time()
-        r = s.run(**kw)
+        ckpt = os.environ.get('NNGP_PK_CKPT')
+        budget = float(os.environ.get('NNGP_PK_BUDGET_S', '0') or 0)
+        extra = {}
+        if ckpt:
+            extra.update(store_int=True, int_dir=ckpt, int_name=tag)
+        if budget > 0:
+            extra['stop_at'] = t0 + budget
+        dumps = sorted(glob.glob(os.path.join(ckpt, tag, f'{tag}_*.npz')),
+                       key=lambda f: int(f.rsplit('_', 1)[1][:-4])) if ckpt else []
+        if dumps:
+            print(f'resuming {tag} from {dumps[-1]}', flush=True)
+            r = s.load_int_dump(dumps[-1], **extra)
+        else:
+            r = s.run(**kw, **extra)
         summ = P.summarise(r)
         summ.update(name=tag, published_K=pk, wall_s=time.time() - t0, Nf_per_slice=s.Nf // s.N,
                     Ng_per_slice=s.Ng // s.N, RK_thresh=s.RK_thresh, run_kwargs={k: v for k, v in kw.items()},
                     spec_hits=r['timings'].get('spec_hits'))
+        if dumps:
+            summ['resumed_from'] = os.path.basename(dumps[-1])
+            summ['runtime_s_incl_earlier_sessions'] = summ['runtime_s']
+        if not r['converged'] and budget > 0 and r['k'] < s.N:
+            tag = tag + '.partial'
         with open(os.path.join(out_dir, tag + '.json'), 'w') as f:
             json.dump(summ, f, indent=1)
         print('RESULT', json.dumps(summ), flush=True)
