@@ -132,3 +132,14 @@ def test_published_burgers59_nngp_paged(gpu):
     (16: iterations 14 and 15 at 1.37 and 1.15 epsilon)."""
     out, pk = _run(gpu, 'burgers59_128_nngp_paged')
     assert out['converged'] and abs(out['K'] - pk) <= 2
+
+
+@LONG
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize('name', ['tomlab_512_para', 'tomlab_256_para'])
+def test_published_tomlab_parareal_k_exact(gpu, name):
+    """TomLab.py Parareal on its unpaged schedule (Nf/N = 1 953 130 / 3 906 250 RK4 steps per
+    slice; the 110-page published schedule is 110x the work): N = 512 K = 180, N = 256 K = 256
+    (= N: the chaotic field never lets it stop early)."""
+    out, pk = _run(gpu, name)
+    assert out['K'] == pk

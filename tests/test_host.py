@@ -1,8 +1,10 @@
 """CPU: host-side logic of the product package (no GPU calls)."""
+import os
+
 import numpy as np
 import pytest
 
-from conftest import golden
+from conftest import ROOT, golden
 
 
 def test_vectorised_draws_equal_the_reference_draw_loop():
@@ -264,3 +266,38 @@ def test_nngp_training_set_attributes_behave_like_the_reference():
     m.x = np.full((5, 3), 2.0)
     m.y = np.full((5, 3), 3.0)
     assert np.all(m.x == 2) and np.all(m.y == 3) and m._dev_xy is None
+
+
+def test_published_builders_restate_the_scripts():
+    """tests/published_k.py's builders (the published K table's configurations, run by
+    tests/test_gpu_published_k.py and bench.py) against the scripts' numbers: steps per slice,
+    tspan, u0 and the paged schedule's page arithmetic (tools/paging_delta.py: FHN-PDE d_x = 10
+    gets 26 pages, 4 % past the slice end; d_x = 16 and TomLab cover the slice)."""
+    import math
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    sys.path.insert(0, os.path.join(ROOT, 'tools'))
+    import published_k as P
+    from paging_delta import pages
+    import nngp_amd as g
+    want = {   # name: (Nf/N, Ng/N, T0, T1)  -- TomLab.py:72-94, Hopf.py:65-69, FHN_PDE.py:34-57, Burgers.py:27-108
+        'tomlab_32_para': (31_250_000, 10, 0, 10), 'tomlab_256_nngp': (3_906_250, 10, 0, 100),
+        'tomlab_512_para': (1_953_130, 10, 0, 100), 'hopf_128_nngp': (13_600_000, 16, -20, 500),
+        'fhn10_512_nngp': (195_315, 3, 0, 150), 'fhn16_512_nngp': (195_325, 25, 0, 1100),
+        'burgers59_128_para': (40_000, 4, 0, 5.9)}
+    for name, (nf, ng, a, b) in want.items():
+        s, kw, pk = P.build(g, name)
+        assert (s.Nf // s.N, s.Ng // s.N) == (nf, ng), name
+        assert s.RK_thresh == float('inf') and pk == P.PUBLISHED_K[tuple([name.split('_')[0], int(name.split('_')[1]),
+                                                                         name.split('_')[2]])]
+        assert float(s.tspan[0]) == a and float(s.tspan[-1]) == b, name
+    s, kw, _ = P.build(g, 'tomlab_256_nngp')
+    u0 = np.array([4.6722764, 5.2437205e-10, -6.4444208e-10])
+    np.testing.assert_array_equal(s.u0, 2 * (u0 + 12) / 24 - 1)   # Systems._tr (new_lib.py:1495-1496)
+    assert kw == dict(model='nngp', nn=18, n_restarts=1, fatol=1e-3, xatol=1e-3, seed=45)
+    for name, n_pages, cover in (('fhn10_512_nngp_paged', 26, 1.04), ('fhn16_512_nngp_paged', 25, 1.0),
+                                 ('tomlab_256_para_paged', 110, 1.0), ('burgers59_128_nngp_paged', 200, 1.0)):
+        s, _, _ = P.build(g, name)
+        span = (float(s.tspan[-1]) - float(s.tspan[0])) / s.N
+        n_p, te = pages(s.Nf // s.N, s.RK_thresh, 0.0, span)
+        assert n_p == n_pages and math.isclose(te / span, cover, rel_tol=1e-9), (name, n_p, te / span)
