@@ -411,7 +411,7 @@ __device__ __forceinline__ void gpf_xcd_map(int lin, int T, int &b, int &t) {
 
 template <bool FULL>   // FULL: the tile's 64 rows exist and pb == LB -- no guards
 __device__ __forceinline__ void gpf_ll_gemm_tile(double *__restrict__ Ab, int ld, int n, int c0, int pb, int r0,
-                                                 bool diag, double *Sa, double *Sb) {
+                                                 bool diag, double *Sa, double *Sb, double *Xd) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int kq = lane >> 4, cl = lane & 15;
     const int sr = tid >> 5, sk = tid & 31;   // staging: rows sr + 8u, column sk of the chunk
@@ -449,6 +449,7 @@ __device__ __forceinline__ void gpf_ll_gemm_tile(double *__restrict__ Ab, int ld
                                                                    0, 0);
         }
     }
+    if (Xd) __syncthreads();                  // the last chunk's operand reads are done: Xd reuses their LDS
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int i = 16 * w + kq + 4 * r;
@@ -457,26 +458,14 @@ __device__ __forceinline__ void gpf_ll_gemm_tile(double *__restrict__ Ab, int ld
             const int j = 16 * cb + cl;
             if (cb < ncb && (FULL || (r0 + i <= n && j < pb)) && (!diag || j <= i)) {
                 double *p = Ab + (size_t)(r0 + i) * ld + c0 + j;
-                *p = *p - acc[cb][r];
+                // the fused diagonal factor's input stays in LDS; the rows below it in tile 0 (the
+                // last, short panel: row n) go back to A for the row solve
+                if (Xd && i < pb) Xd[i * (LB + 1) + j] = *p - acc[cb][r];
+                else *p = *p - acc[cb][r];
             }
         }
     }
 #undef GPF_LL_LOAD
-}
-
-__global__ void __launch_bounds__(256, 2) gpf_ll_gemm_kernel(double *__restrict__ A, int n, int c0, int pb,
-                                                              const int32_t *__restrict__ fail, int T, int nmat) {
-    int b, t;
-    gpf_xcd_map(blockIdx.x + blockIdx.y * T, T, b, t);
-    if (b >= nmat || fail[b]) return;
-    const int ld = n + 1;
-    double *Ab = A + (size_t)b * ld * ld;
-    const int r0 = c0 + LB * t;
-    __shared__ double Sa[LB * LKS], Sb[LB * LKS];
-    if (r0 + LB - 1 <= n && pb == LB)
-        gpf_ll_gemm_tile<true>(Ab, ld, n, c0, pb, r0, t == 0, Sa, Sb);
-    else
-        gpf_ll_gemm_tile<false>(Ab, ld, n, c0, pb, r0, t == 0, Sa, Sb);
 }
 
 template <bool FMA>
@@ -485,21 +474,13 @@ __device__ __forceinline__ double gpf_msub(double x, double a, double b) {   // 
     else return x - a * b;
 }
 
-// The 64x64 diagonal block of one matrix per wave (lane i = row i, right-looking by columns:
+// The 64x64 diagonal block of one matrix on one wave (lane i = row i, right-looking by columns:
 // L_jj = sqrt(a_jj), L_ij = a_ij * (1/L_jj), a_ik -= L_ij L_kj for k > j), the column broadcast
-// through LDS.  Lanes i < k carry garbage in a[k] (the upper triangle), never stored.
+// through LDS.  Lanes i < k carry garbage in a[k] (the upper triangle), never stored.  Leaves L11
+// (column-major) and 1/L_jj in Lpan[b], or sets fail[b].
 template <bool FMA>
-__global__ void __launch_bounds__(64) gpf_ll_diag_kernel(const double *__restrict__ A, int n, int c0, int pb,
-                                                          int32_t *__restrict__ fail, double *__restrict__ Lpan,
-                                                          int nmat) {
-    const int b = blockIdx.x;
-    if (b >= nmat || fail[b]) return;
-    const int i = threadIdx.x, ld = n + 1;
-    const double *Ab = A + (size_t)b * ld * ld;
-    __shared__ __attribute__((aligned(16))) double col[LB];
-    double a[LB];
-#pragma unroll
-    for (int k = 0; k < LB; k++) a[k] = (i < pb && k <= i) ? Ab[(size_t)(c0 + i) * ld + c0 + k] : 0.0;
+__device__ __forceinline__ void gpf_ll_factor(double (&a)[LB], int i, int pb, double *col, int b,
+                                              int32_t *__restrict__ fail, double *__restrict__ Lpan) {
     bool bad = false;
     double myr = 1.0;
 #pragma unroll
@@ -527,6 +508,53 @@ __global__ void __launch_bounds__(64) gpf_ll_diag_kernel(const double *__restric
 #pragma unroll
     for (int k = 0; k < LB; k++) Lb[k * LB + i] = (i < pb && k <= i) ? a[k] : 0.0;
     Lb[LB * LB + i] = myr;
+}
+
+template <bool FMA>
+__global__ void __launch_bounds__(64) gpf_ll_diag_kernel(const double *__restrict__ A, int n, int c0, int pb,
+                                                          int32_t *__restrict__ fail, double *__restrict__ Lpan,
+                                                          int nmat) {
+    const int b = blockIdx.x;
+    if (b >= nmat || fail[b]) return;
+    const int i = threadIdx.x, ld = n + 1;
+    const double *Ab = A + (size_t)b * ld * ld;
+    __shared__ __attribute__((aligned(16))) double col[LB];
+    double a[LB];
+#pragma unroll
+    for (int k = 0; k < LB; k++) a[k] = (i < pb && k <= i) ? Ab[(size_t)(c0 + i) * ld + c0 + k] : 0.0;
+    gpf_ll_factor<FMA>(a, i, pb, col, b, fail, Lpan);
+}
+
+// FUSED: the diagonal tile's workgroup (dispatched before the matrix's other tiles: gpf_xcd_map
+// gives tile 0 the matrix's lowest linear id) leaves its updated block in LDS and factors it on
+// wave 0 -- gpf_ll_diag_kernel's arithmetic on the same values, one launch fewer per panel
+template <bool FUSED, bool FMA>
+__global__ void __launch_bounds__(256, 2) gpf_ll_gemm_kernel(double *__restrict__ A, int n, int c0, int pb,
+                                                              int32_t *__restrict__ fail, double *__restrict__ Lpan,
+                                                              int T, int nmat) {
+    int b, t;
+    gpf_xcd_map(blockIdx.x + blockIdx.y * T, T, b, t);
+    if (b >= nmat || fail[b]) return;
+    const int ld = n + 1;
+    double *Ab = A + (size_t)b * ld * ld;
+    const int r0 = c0 + LB * t;
+    __shared__ __attribute__((aligned(16))) double S[2 * LB * LKS];   // Sa | Sb; then the fused factor's block
+    double *Xd = (FUSED && t == 0) ? S : nullptr;
+    if (r0 + LB - 1 <= n && pb == LB)
+        gpf_ll_gemm_tile<true>(Ab, ld, n, c0, pb, r0, t == 0, S, S + LB * LKS, Xd);
+    else
+        gpf_ll_gemm_tile<false>(Ab, ld, n, c0, pb, r0, t == 0, S, S + LB * LKS, Xd);
+    if constexpr (FUSED) {
+        if (t != 0) return;
+        __syncthreads();
+        if (threadIdx.x >= 64) return;
+        __shared__ __attribute__((aligned(16))) double col[LB];
+        const int i = threadIdx.x;
+        double a[LB];
+#pragma unroll
+        for (int k = 0; k < LB; k++) a[k] = (i < pb && k <= i) ? Xd[i * (LB + 1) + k] : 0.0;
+        gpf_ll_factor<FMA>(a, i, pb, col, b, fail, Lpan);
+    }
 }
 
 template <bool FMA>
@@ -707,7 +735,8 @@ int gpfull_mean(const double *X, int64_t rows, int d, const double *q, const dou
 // The batched -LML pipeline for nb points (device pts), D2 [n][n] given; A: nb*(n+1)^2 scratch.
 // Factor order: NNGP_GPF_ORDER=0 (default) the left-looking 64-column panels, 1 the right-looking
 // 32-column order (rounds 3-5); NNGP_GPF_FMA=1 fuses the diagonal factor's and the row solve's
-// updates (left-looking order only).
+// updates (left-looking order only); NNGP_GPF_FUSE=0 factors the diagonal block in its own launch
+// instead of in the panel GEMM's tile-0 workgroups (bitwise the same).
 static int gpf_eval(const double *D2, int n, const double *Y, int d, const GPPoint *pts, int nb, double *A,
                     int32_t *fail, double *fval, double *alpha_out, double *Lpan, hipStream_t st) {
     NNGP_HIP_CHECK(hipMemsetAsync(fail, 0, sizeof(int32_t) * nb, st));
@@ -716,17 +745,29 @@ static int gpf_eval(const double *D2, int n, const double *Y, int d, const GPPoi
     NNGP_LAUNCH_CHECK();
     const unsigned ny8 = (unsigned)((nb + 7) / 8 * 8);   // grid y padded: XCD order
     if (env_int("NNGP_GPF_ORDER", 0) == 0) {
-        const bool fma = env_int("NNGP_GPF_FMA", 0) != 0;
+        const bool fma = env_int("NNGP_GPF_FMA", 0) != 0, fused = env_int("NNGP_GPF_FUSE", 1) != 0;
         for (int c0 = 0; c0 < n; c0 += LB) {
             const int pb = std::min(LB, n - c0);
-            if (c0 > 0) {
-                const int T = (n + 1 - c0 + LB - 1) / LB;
-                hipLaunchKernelGGL(gpf_ll_gemm_kernel, dim3(T, ny8), dim3(256), 0, st, A, n, c0, pb, fail, T, nb);
+            const int T = (n + 1 - c0 + LB - 1) / LB;
+            const dim3 gg((unsigned)T, ny8);
+            if (c0 > 0 && fused) {   // panel GEMM with the diagonal factor in its tile-0 workgroups
+                if (fma)
+                    hipLaunchKernelGGL((gpf_ll_gemm_kernel<true, true>), gg, dim3(256), 0, st, A, n, c0, pb, fail, Lpan,
+                                       T, nb);
+                else
+                    hipLaunchKernelGGL((gpf_ll_gemm_kernel<true, false>), gg, dim3(256), 0, st, A, n, c0, pb, fail,
+                                       Lpan, T, nb);
+            } else {
+                if (c0 > 0)
+                    hipLaunchKernelGGL((gpf_ll_gemm_kernel<false, false>), gg, dim3(256), 0, st, A, n, c0, pb, fail,
+                                       Lpan, T, nb);
+                if (fma)
+                    hipLaunchKernelGGL(gpf_ll_diag_kernel<true>, dim3(nb), dim3(64), 0, st, A, n, c0, pb, fail, Lpan,
+                                       nb);
+                else
+                    hipLaunchKernelGGL(gpf_ll_diag_kernel<false>, dim3(nb), dim3(64), 0, st, A, n, c0, pb, fail, Lpan,
+                                       nb);
             }
-            if (fma)
-                hipLaunchKernelGGL(gpf_ll_diag_kernel<true>, dim3(nb), dim3(64), 0, st, A, n, c0, pb, fail, Lpan, nb);
-            else
-                hipLaunchKernelGGL(gpf_ll_diag_kernel<false>, dim3(nb), dim3(64), 0, st, A, n, c0, pb, fail, Lpan, nb);
             const int TR = (n + 1 - c0 - pb + 255) / 256;   // >= 1: row n is always below
             if (fma)
                 hipLaunchKernelGGL(gpf_ll_rows_kernel<true>, dim3(TR, ny8), dim3(256), 0, st, A, n, c0, pb, fail, Lpan,

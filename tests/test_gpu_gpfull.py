@@ -72,7 +72,8 @@ ORDERS = {'ll64': {'NNGP_GPF_ORDER': '0', 'NNGP_GPF_FMA': '0'}, 'll64_fma': {'NN
 def test_gpfull_lml_and_weights_vs_oracle(gpu, n, order, monkeypatch):
     """Panel edges (31/32/33 and 63/64/65), several panels, and a 600-row set (the size GParareal
     reaches), in every factor order (NNGP_GPF_ORDER / NNGP_GPF_FMA; each against the oracle, as
-    they round differently); and a one-matrix slab (NNGP_GPF_SLAB_MB) bitwise the whole batch."""
+    they round differently); a one-matrix slab (NNGP_GPF_SLAB_MB) and the unfused diagonal factor
+    (NNGP_GPF_FUSE=0) bitwise the defaults."""
     import torch
     for k, v in ORDERS[order].items():
         monkeypatch.setenv(k, v)
@@ -86,6 +87,10 @@ def test_gpfull_lml_and_weights_vs_oracle(gpu, n, order, monkeypatch):
     monkeypatch.setenv('NNGP_GPF_SLAB_MB', str(max(1, 8 * (n + 1) ** 2 >> 20)))   # one matrix per chunk
     fv1, al1 = _lml(gpu, torch, x, y, coords, jit, thetas, alpha=True)
     assert np.array_equal(fv1, fv) and np.array_equal(np.nan_to_num(al1[:3]), np.nan_to_num(al[:3]))
+    if order != 'rl32':   # the diagonal factor in its own launch: bitwise the fused one
+        monkeypatch.setenv('NNGP_GPF_FUSE', '0')
+        fv2, al2 = _lml(gpu, torch, x, y, coords, jit, thetas, alpha=True)
+        assert np.array_equal(fv2, fv) and np.array_equal(np.nan_to_num(al2[:3]), np.nan_to_num(al[:3]))
     # sigma_x = 0: NaN kernel -> failed Cholesky -> +inf (the reference would raise from
     # solve_triangular's finite check here, so there is no reference value to compare with)
     assert np.isinf(fv[3]) and fv[3] > 0

@@ -54,11 +54,11 @@ KNOBS = [
 # ::test_knn_streaming_select_vs_oracle runs every case with and without the LDS key cache)
 # NNGP_G_SIDE (an unsplit PDE sweep, i.e. without speculation: test_gpu_parareal.py
 # ::test_g_side_stream_is_bitwise)
-# NNGP_GPF_SLAB_MB / NNGP_GPF_ORDER / NNGP_GPF_FMA (the full-GP factorisation, not on the nnGP
+# NNGP_GPF_SLAB_MB / NNGP_GPF_FUSE / NNGP_GPF_ORDER / NNGP_GPF_FMA (the full-GP factorisation, not on the nnGP
 # path: test_gpu_gpfull.py::test_gpfull_lml_and_weights_vs_oracle -- the slab bitwise, the two
 # orders and FMA each against the oracle to tolerance, as they change the Cholesky's rounding)
 COVERED_ELSEWHERE = ['NNGP_COMM_TIMEOUT_S', 'NNGP_KEY_LDS', 'NNGP_G_SIDE', 'NNGP_GPF_SLAB_MB', 'NNGP_GPF_ORDER',
-                     'NNGP_GPF_FMA']
+                     'NNGP_GPF_FMA', 'NNGP_GPF_FUSE']
 
 
 @pytest.mark.parametrize('case,knob,value', KNOBS)

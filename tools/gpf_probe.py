@@ -37,7 +37,10 @@ def run(n, npts, d=3, reps=3):
     fv = np.empty(npts)
     ip, dp = ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)
     out = {}
+    only = os.environ.get('GPF_PROBE_ORDERS')
     for name, env in ORDERS:
+        if only and name not in only.split(','):
+            continue
         os.environ.update(env)
         ts = []
         for _ in range(reps):
@@ -53,6 +56,8 @@ def run(n, npts, d=3, reps=3):
         out[name] = fv.copy()
         print(f'rows={n} points={npts} {name:9s}: {t * 1e3:9.2f} ms  {fl / t / 1e12:6.2f} TF/s executed Cholesky '
               f'({np.isfinite(fv).sum()} finite)', flush=True)
+    if 'rl32' not in out:
+        return
     ref = out['rl32']
     for name in ('ll64', 'll64_fma'):
         a = out[name]
