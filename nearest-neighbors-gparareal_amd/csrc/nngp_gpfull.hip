@@ -398,7 +398,7 @@ __global__ void __launch_bounds__(256, 3) gpf_update_kernel(double *__restrict__
 // Nelder-Mead round has 3 launches per 64 columns instead of per 32.
 static constexpr int LB = 64;                // panel width
 static constexpr int LPS64 = LB * LB + LB;   // Lpan doubles per matrix: L11 column-major | 1/L_jj
-static constexpr int LKC = 32;               // k chunk of the panel GEMM
+static constexpr int LKC = 32;               // k chunk of the panel GEMM (c0 is a multiple: no tail; 64 measured slower: 68 KB of LDS and 237 VGPRs left 2 workgroups per CU instead of 3)
 static constexpr int LKS = LKC + 2;          // its LDS row stride (the gpf_update_tile operand pattern)
 
 // (matrix, tile) of linear workgroup `lin`: workgroups go round-robin over the 8 XCDs, the k-th of
@@ -409,31 +409,58 @@ __device__ __forceinline__ void gpf_xcd_map(int lin, int T, int &b, int &t) {
     t = kx % T;
 }
 
-template <bool FULL>   // FULL: the tile's 64 rows exist and pb == LB -- no guards
+// The point's original matrix entry, computed where the left-looking order first reads it (each
+// column block exactly once: the panel GEMM's epilogue, or panel 0's factor and row solve) instead
+// of built in HBM beforehand: gpf_build_kernel's expression (kernel_np, models.py:302-304, + 10^jitter
+// on the diagonal), row n = y.  At Burgers N = 128 sizes the build kernel wrote 2.6 GB per round and
+// the factor read it back.  r, c must be inside the matrix (callers clamp).
+__device__ __forceinline__ double gpf_entry(const double *__restrict__ D2, int n, const double *__restrict__ Y, int d,
+                                            const GPPoint &p, int r, int c) {
+    const double dv = D2[(size_t)min(r, n - 1) * n + c];   // both loads unconditional (no branch per entry)
+    const double yv = Y[(size_t)c * d + p.coord];
+    double v = p.psy * exp(p.c * dv);
+    v = (r == c) ? v + p.jp : v;
+    return (r == n) ? yv : v;
+}
+
+// Every guarded access below loads from a clamped (valid) address and selects zero afterwards:
+// a load under a lane condition compiles to a branch with its own wait, and a row solve whose 65
+// loads were serialised that way took ~90 us per workgroup (profiles/r06/gparareal).
+// FULL: the tile's 64 rows exist and pb == LB -- no guards.  DIAG: tile 0 (its B rows are its own A
+// rows; only j <= i is stored).  Both compile-time, and every MFMA block and original entry is
+// computed for every tile (the diagonal tile's upper blocks are wasted work): a branch around the
+// MFMAs or the loads made the compiler wait for the next chunk's prefetch before the MFMAs.
+template <bool FULL, bool DIAG>
 __device__ __forceinline__ void gpf_ll_gemm_tile(double *__restrict__ Ab, int ld, int n, int c0, int pb, int r0,
-                                                 bool diag, double *Sa, double *Sb, double *Xd) {
+                                                 double *Sa, double *Sb, double *Xd,
+                                                 const double *__restrict__ D2, const double *__restrict__ Y, int d,
+                                                 const GPPoint &pt) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int kq = lane >> 4, cl = lane & 15;
-    const int sr = tid >> 5, sk = tid & 31;   // staging: rows sr + 8u, column sk of the chunk
-    double *SB = diag ? Sa : Sb;              // the diagonal tile's B rows are its own A rows
-    double va[8], vb[8];
+    constexpr int SU = LB * LKC / 256;        // staged doubles per thread and operand
+    const int sr = tid / LKC, sk = tid % LKC; // staging: rows sr + (256 / LKC) u, column sk of the chunk
+    constexpr int RS = 256 / LKC;
+    double *SB = DIAG ? Sa : Sb;              // the diagonal tile's B rows are its own A rows
+    double va[SU], vb[SU];
 #define GPF_LL_LOAD(kk)                                                                                  \
-    _Pragma("unroll") for (int u = 0; u < 8; u++) {                                                    \
-        const int rr = sr + 8 * u;                                                                     \
-        va[u] = (FULL || r0 + rr <= n) ? Ab[(size_t)(r0 + rr) * ld + (kk) + sk] : 0.0;                 \
-        vb[u] = (!diag && (FULL || rr < pb)) ? Ab[(size_t)(c0 + rr) * ld + (kk) + sk] : 0.0;           \
+    _Pragma("unroll") for (int u = 0; u < SU; u++) {                                                   \
+        const int rr = sr + RS * u;                                                                    \
+        const int ra = FULL ? r0 + rr : min(r0 + rr, n), rb = FULL ? rr : min(rr, pb - 1);             \
+        const double x = Ab[(size_t)ra * ld + (kk) + sk];                                              \
+        const double y = DIAG ? 0.0 : Ab[(size_t)(c0 + rb) * ld + (kk) + sk];                          \
+        va[u] = (FULL || r0 + rr <= n) ? x : 0.0;                                                      \
+        vb[u] = (FULL || rr < pb) ? y : 0.0;                                                           \
     }
     f64x4 acc[4];
 #pragma unroll
     for (int cb = 0; cb < 4; cb++) acc[cb] = f64x4{0.0, 0.0, 0.0, 0.0};
-    const int ncb = diag ? w + 1 : 4;         // the diagonal tile: column blocks at or left of the wave's rows
     GPF_LL_LOAD(0)
     for (int kk = 0; kk < c0; kk += LKC) {
         __syncthreads();                      // the previous chunk's operand reads are done
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-            Sa[(sr + 8 * u) * LKS + sk] = va[u];
-            if (!diag) Sb[(sr + 8 * u) * LKS + sk] = vb[u];
+        for (int u = 0; u < SU; u++) {
+            Sa[(sr + RS * u) * LKS + sk] = va[u];
+            if constexpr (!DIAG) Sb[(sr + RS * u) * LKS + sk] = vb[u];
         }
         __syncthreads();
         if (kk + LKC < c0) {                  // the next chunk's loads fly under this chunk's MFMAs
@@ -444,9 +471,18 @@ __device__ __forceinline__ void gpf_ll_gemm_tile(double *__restrict__ Ab, int ld
             const double av = Sa[(16 * w + cl) * LKS + k + kq];
 #pragma unroll
             for (int cb = 0; cb < 4; cb++)
-                if (cb < ncb)
-                    acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, SB[(16 * cb + cl) * LKS + k + kq], acc[cb], 0,
-                                                                   0, 0);
+                acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, SB[(16 * cb + cl) * LKS + k + kq], acc[cb], 0, 0, 0);
+        }
+    }
+    // the original entries of this tile's panel columns, all computed before any store
+    double ov[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int i = 16 * w + kq + 4 * r;
+#pragma unroll
+        for (int cb = 0; cb < 4; cb++) {
+            const int j = 16 * cb + cl;
+            ov[cb][r] = gpf_entry(D2, n, Y, d, pt, FULL ? r0 + i : min(r0 + i, n), c0 + (FULL ? j : min(j, pb - 1)));
         }
     }
     if (Xd) __syncthreads();                  // the last chunk's operand reads are done: Xd reuses their LDS
@@ -456,12 +492,12 @@ __device__ __forceinline__ void gpf_ll_gemm_tile(double *__restrict__ Ab, int ld
 #pragma unroll
         for (int cb = 0; cb < 4; cb++) {
             const int j = 16 * cb + cl;
-            if (cb < ncb && (FULL || (r0 + i <= n && j < pb)) && (!diag || j <= i)) {
-                double *p = Ab + (size_t)(r0 + i) * ld + c0 + j;
+            if ((FULL || (r0 + i <= n && j < pb)) && (!DIAG || j <= i)) {
+                const double v = ov[cb][r] - acc[cb][r];
                 // the fused diagonal factor's input stays in LDS; the rows below it in tile 0 (the
-                // last, short panel: row n) go back to A for the row solve
-                if (Xd && i < pb) Xd[i * (LB + 1) + j] = *p - acc[cb][r];
-                else *p = *p - acc[cb][r];
+                // last, short panel: row n) go to A for the row solve
+                if (Xd && i < pb) Xd[i * (LB + 1) + j] = v;
+                else Ab[(size_t)(r0 + i) * ld + c0 + j] = v;
             }
         }
     }
@@ -510,18 +546,32 @@ __device__ __forceinline__ void gpf_ll_factor(double (&a)[LB], int i, int pb, do
     Lb[LB * LB + i] = myr;
 }
 
+// FLY: panel 0, the block's original entries computed (gpf_entry); else read from A (the panel
+// GEMM left them there, NNGP_GPF_FUSE=0)
 template <bool FMA>
 __global__ void __launch_bounds__(64) gpf_ll_diag_kernel(const double *__restrict__ A, int n, int c0, int pb,
                                                           int32_t *__restrict__ fail, double *__restrict__ Lpan,
-                                                          int nmat) {
+                                                          int nmat, const double *__restrict__ D2,
+                                                          const double *__restrict__ Y, int d,
+                                                          const GPPoint *__restrict__ pts) {
     const int b = blockIdx.x;
     if (b >= nmat || fail[b]) return;
     const int i = threadIdx.x, ld = n + 1;
     const double *Ab = A + (size_t)b * ld * ld;
     __shared__ __attribute__((aligned(16))) double col[LB];
+    const bool fly = (c0 == 0);
+    const GPPoint pt = pts[b];
+    const int ic = min(i, pb - 1);
     double a[LB];
+    if (fly) {
 #pragma unroll
-    for (int k = 0; k < LB; k++) a[k] = (i < pb && k <= i) ? Ab[(size_t)(c0 + i) * ld + c0 + k] : 0.0;
+        for (int k = 0; k < LB; k++) a[k] = gpf_entry(D2, n, Y, d, pt, c0 + ic, c0 + min(k, ic));
+    } else {
+#pragma unroll
+        for (int k = 0; k < LB; k++) a[k] = Ab[(size_t)(c0 + ic) * ld + c0 + min(k, ic)];
+    }
+#pragma unroll
+    for (int k = 0; k < LB; k++) a[k] = (i < pb && k <= i) ? a[k] : 0.0;
     gpf_ll_factor<FMA>(a, i, pb, col, b, fail, Lpan);
 }
 
@@ -531,19 +581,27 @@ __global__ void __launch_bounds__(64) gpf_ll_diag_kernel(const double *__restric
 template <bool FUSED, bool FMA>
 __global__ void __launch_bounds__(256, 2) gpf_ll_gemm_kernel(double *__restrict__ A, int n, int c0, int pb,
                                                               int32_t *__restrict__ fail, double *__restrict__ Lpan,
-                                                              int T, int nmat) {
+                                                              int T, int nmat, const double *__restrict__ D2,
+                                                              const double *__restrict__ Y, int d,
+                                                              const GPPoint *__restrict__ pts) {
     int b, t;
     gpf_xcd_map(blockIdx.x + blockIdx.y * T, T, b, t);
     if (b >= nmat || fail[b]) return;
     const int ld = n + 1;
     double *Ab = A + (size_t)b * ld * ld;
     const int r0 = c0 + LB * t;
+    const GPPoint pt = pts[b];
     __shared__ __attribute__((aligned(16))) double S[2 * LB * LKS];   // Sa | Sb; then the fused factor's block
+    static_assert(2 * LB * LKS >= LB * (LB + 1), "the fused factor's block reuses the operand LDS");
     double *Xd = (FUSED && t == 0) ? S : nullptr;
-    if (r0 + LB - 1 <= n && pb == LB)
-        gpf_ll_gemm_tile<true>(Ab, ld, n, c0, pb, r0, t == 0, S, S + LB * LKS, Xd);
-    else
-        gpf_ll_gemm_tile<false>(Ab, ld, n, c0, pb, r0, t == 0, S, S + LB * LKS, Xd);
+    const bool full = r0 + LB - 1 <= n && pb == LB;
+    if (t == 0) {
+        if (full) gpf_ll_gemm_tile<true, true>(Ab, ld, n, c0, pb, r0, S, S + LB * LKS, Xd, D2, Y, d, pt);
+        else gpf_ll_gemm_tile<false, true>(Ab, ld, n, c0, pb, r0, S, S + LB * LKS, Xd, D2, Y, d, pt);
+    } else {
+        if (full) gpf_ll_gemm_tile<true, false>(Ab, ld, n, c0, pb, r0, S, S + LB * LKS, nullptr, D2, Y, d, pt);
+        else gpf_ll_gemm_tile<false, false>(Ab, ld, n, c0, pb, r0, S, S + LB * LKS, nullptr, D2, Y, d, pt);
+    }
     if constexpr (FUSED) {
         if (t != 0) return;
         __syncthreads();
@@ -557,10 +615,16 @@ __global__ void __launch_bounds__(256, 2) gpf_ll_gemm_kernel(double *__restrict_
     }
 }
 
+// The rows below the diagonal block: x L11^T = a by substitution (dtrsm's right-looking order with
+// 1/L_jj), one lane per row, staged through LDS 16 columns at a time (coalesced).  Panel 0 (FLY)
+// computes the rows' original entries instead of reading them.
 template <bool FMA>
 __global__ void __launch_bounds__(256) gpf_ll_rows_kernel(double *__restrict__ A, int n, int c0, int pb,
                                                            const int32_t *__restrict__ fail,
-                                                           const double *__restrict__ Lpan, int T, int nmat) {
+                                                           const double *__restrict__ Lpan, int T, int nmat,
+                                                           const double *__restrict__ D2,
+                                                           const double *__restrict__ Y, int d,
+                                                           const GPPoint *__restrict__ pts) {
     int b, t;
     gpf_xcd_map(blockIdx.x + blockIdx.y * T, T, b, t);
     if (b >= nmat || fail[b]) return;
@@ -570,29 +634,64 @@ __global__ void __launch_bounds__(256) gpf_ll_rows_kernel(double *__restrict__ A
     __shared__ double X[4][LB * 17];                           // per wave: 64 rows x 16 columns
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const double *Lsrc = Lpan + (size_t)b * LPS64;
-    for (int e = tid; e < LPS64; e += 256) L[e] = Lsrc[e];
+    const int rw = c0 + pb + 256 * t + 64 * w;   // this wave's first row
+    const bool fly = (c0 == 0), act = rw <= n;
+    const GPPoint pt = pts[b];
+    double *Xw = X[w];
+    // 16 columns of the wave's 64 rows per round, coalesced; round q + 1's loads are issued before
+    // round q goes through LDS, and round 0's before the L11 copy (software-pipelined: each round
+    // used to wait out a full memory latency)
+    double sv[16], sn[16];
+#define GPF_ROWS_STAGE(dst, q)                                                                          \
+    if (fly) {                                                                                        \
+        _Pragma("unroll") for (int v = 0; v < 16; v++) {                                               \
+            const int e = lane + 64 * v, rr = e >> 4, k = 16 * (q) + (e & 15);                         \
+            dst[v] = gpf_entry(D2, n, Y, d, pt, min(rw + rr, n), min(k, pb - 1));                      \
+        }                                                                                             \
+    } else {                                                                                          \
+        _Pragma("unroll") for (int v = 0; v < 16; v++) {                                               \
+            const int e = lane + 64 * v, rr = e >> 4, k = 16 * (q) + (e & 15);                         \
+            dst[v] = Ab[(size_t)min(rw + rr, n) * ld + c0 + min(k, pb - 1)];                           \
+        }                                                                                             \
+    }
+    if (act) {
+        GPF_ROWS_STAGE(sv, 0)
+    }
+    {   // all 17 loads issued before the first LDS store
+        constexpr int NL = (LPS64 + 255) / 256;
+        double lv[NL];
+#pragma unroll
+        for (int u = 0; u < NL; u++) lv[u] = Lsrc[min(tid + 256 * u, LPS64 - 1)];
+#pragma unroll
+        for (int u = 0; u < NL; u++)
+            if (tid + 256 * u < LPS64) L[tid + 256 * u] = lv[u];
+    }
     __syncthreads();
     if (t == 0)   // L11 into A's diagonal block, coalesced along the rows
         for (int e = tid; e < LB * LB; e += 256) {
             const int ii = e >> 6, k = e & 63;
             if (k <= ii && ii < pb) Ab[(size_t)(c0 + ii) * ld + c0 + k] = L[k * LB + ii];
         }
-    const int rw = c0 + pb + 256 * t + 64 * w;   // this wave's first row
-    if (rw > n) return;                          // (no barrier follows)
-    double *Xw = X[w];
+    if (!act) return;                            // (no barrier follows)
     double x[LB];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {   // stage 16 columns of the wave's 64 rows, coalesced
+    for (int q = 0; q < 4; q++) {
+        if (q < 3) {
+            GPF_ROWS_STAGE(sn, q + 1)
+        }
 #pragma unroll
         for (int v = 0; v < 16; v++) {
             const int e = lane + 64 * v, rr = e >> 4, k = 16 * q + (e & 15);
-            Xw[rr * 17 + (e & 15)] = (rw + rr <= n && k < pb) ? Ab[(size_t)(rw + rr) * ld + c0 + k] : 0.0;
+            Xw[rr * 17 + (e & 15)] = (rw + rr <= n && k < pb) ? sv[v] : 0.0;
         }
         wave_sync_lds();
 #pragma unroll
         for (int c = 0; c < 16; c++) x[16 * q + c] = Xw[lane * 17 + c];
         wave_sync_lds();
+#pragma unroll
+        for (int v = 0; v < 16; v++) sv[v] = sn[v];
     }
+#undef GPF_ROWS_STAGE
 #pragma unroll
     for (int j = 0; j < LB; j++) {
         if (j < pb) {
@@ -735,16 +834,20 @@ int gpfull_mean(const double *X, int64_t rows, int d, const double *q, const dou
 // The batched -LML pipeline for nb points (device pts), D2 [n][n] given; A: nb*(n+1)^2 scratch.
 // Factor order: NNGP_GPF_ORDER=0 (default) the left-looking 64-column panels, 1 the right-looking
 // 32-column order (rounds 3-5); NNGP_GPF_FMA=1 fuses the diagonal factor's and the row solve's
-// updates (left-looking order only); NNGP_GPF_FUSE=0 factors the diagonal block in its own launch
+// updates a - l*l' into one FMA (left-looking order only; ~5 % faster, but the FHN-ODE GParareal
+// iterates then part from the reference's by 1.9e-5, against 1e-6 unfused: not the default); NNGP_GPF_FUSE=0 factors the diagonal block in its own launch
 // instead of in the panel GEMM's tile-0 workgroups (bitwise the same).
 static int gpf_eval(const double *D2, int n, const double *Y, int d, const GPPoint *pts, int nb, double *A,
                     int32_t *fail, double *fval, double *alpha_out, double *Lpan, hipStream_t st) {
     NNGP_HIP_CHECK(hipMemsetAsync(fail, 0, sizeof(int32_t) * nb, st));
-    const unsigned bx = (unsigned)((n + GPF_BROWS - 1) / GPF_BROWS + 1);   // + the y row's block
-    hipLaunchKernelGGL(gpf_build_kernel, dim3(bx, nb), dim3(256), 0, st, D2, n, Y, d, pts, A, fail);
-    NNGP_LAUNCH_CHECK();
+    const bool ll = env_int("NNGP_GPF_ORDER", 0) == 0;
+    if (!ll) {   // the left-looking order computes each entry where it first reads it (gpf_entry)
+        const unsigned bx = (unsigned)((n + GPF_BROWS - 1) / GPF_BROWS + 1);   // + the y row's block
+        hipLaunchKernelGGL(gpf_build_kernel, dim3(bx, nb), dim3(256), 0, st, D2, n, Y, d, pts, A, fail);
+        NNGP_LAUNCH_CHECK();
+    }
     const unsigned ny8 = (unsigned)((nb + 7) / 8 * 8);   // grid y padded: XCD order
-    if (env_int("NNGP_GPF_ORDER", 0) == 0) {
+    if (ll) {
         const bool fma = env_int("NNGP_GPF_FMA", 0) != 0, fused = env_int("NNGP_GPF_FUSE", 1) != 0;
         for (int c0 = 0; c0 < n; c0 += LB) {
             const int pb = std::min(LB, n - c0);
@@ -753,28 +856,28 @@ static int gpf_eval(const double *D2, int n, const double *Y, int d, const GPPoi
             if (c0 > 0 && fused) {   // panel GEMM with the diagonal factor in its tile-0 workgroups
                 if (fma)
                     hipLaunchKernelGGL((gpf_ll_gemm_kernel<true, true>), gg, dim3(256), 0, st, A, n, c0, pb, fail, Lpan,
-                                       T, nb);
+                                       T, nb, D2, Y, d, pts);
                 else
                     hipLaunchKernelGGL((gpf_ll_gemm_kernel<true, false>), gg, dim3(256), 0, st, A, n, c0, pb, fail,
-                                       Lpan, T, nb);
+                                       Lpan, T, nb, D2, Y, d, pts);
             } else {
                 if (c0 > 0)
                     hipLaunchKernelGGL((gpf_ll_gemm_kernel<false, false>), gg, dim3(256), 0, st, A, n, c0, pb, fail,
-                                       Lpan, T, nb);
+                                       Lpan, T, nb, D2, Y, d, pts);
                 if (fma)
                     hipLaunchKernelGGL(gpf_ll_diag_kernel<true>, dim3(nb), dim3(64), 0, st, A, n, c0, pb, fail, Lpan,
-                                       nb);
+                                       nb, D2, Y, d, pts);
                 else
                     hipLaunchKernelGGL(gpf_ll_diag_kernel<false>, dim3(nb), dim3(64), 0, st, A, n, c0, pb, fail, Lpan,
-                                       nb);
+                                       nb, D2, Y, d, pts);
             }
             const int TR = (n + 1 - c0 - pb + 255) / 256;   // >= 1: row n is always below
             if (fma)
                 hipLaunchKernelGGL(gpf_ll_rows_kernel<true>, dim3(TR, ny8), dim3(256), 0, st, A, n, c0, pb, fail, Lpan,
-                                   TR, nb);
+                                   TR, nb, D2, Y, d, pts);
             else
                 hipLaunchKernelGGL(gpf_ll_rows_kernel<false>, dim3(TR, ny8), dim3(256), 0, st, A, n, c0, pb, fail,
-                                   Lpan, TR, nb);
+                                   Lpan, TR, nb, D2, Y, d, pts);
         }
     } else {
         for (int p0 = 0; p0 < n; p0 += GPB) {

@@ -32,7 +32,11 @@ def run(n, npts, d=3, reps=3):
     X = torch.tensor(x, device='cuda')
     Y = torch.tensor(y, device='cuda')
     c = np.ascontiguousarray(np.arange(npts) % d, dtype=np.int32)
-    jx = np.ascontiguousarray(-20.0 + (np.arange(npts) % 9), dtype=float)
+    # GParareal's jitters (-20..-12) leave most of these matrices failing part-way (their later panels
+    # are skipped, so the rate below would overstate the work); GPF_PROBE_JITTER=-2 makes every
+    # factorisation complete, so executed = points x (rows+1)^3 / 3 exactly
+    jit = os.environ.get('GPF_PROBE_JITTER')
+    jx = np.ascontiguousarray(np.full(npts, float(jit)) if jit else -20.0 + (np.arange(npts) % 9), dtype=float)
     th = np.ascontiguousarray(np.column_stack([0.3 + 0.5 * rng.random(npts), 0.5 + rng.random(npts)]))
     fv = np.empty(npts)
     ip, dp = ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)
@@ -59,7 +63,7 @@ def run(n, npts, d=3, reps=3):
     if 'rl32' not in out:
         return
     ref = out['rl32']
-    for name in ('ll64', 'll64_fma'):
+    for name in [k for k in ('ll64', 'll64_fma') if k in out]:
         a = out[name]
         both = np.isfinite(a) & np.isfinite(ref)
         rel = np.abs(a[both] - ref[both]) / np.maximum(1, np.abs(ref[both])) if both.any() else np.zeros(1)
