@@ -143,3 +143,12 @@ def test_published_tomlab_parareal_k_exact(gpu, name):
     (= N: the chaotic field never lets it stop early)."""
     out, pk = _run(gpu, name)
     assert out['K'] == pk
+
+
+@LONG
+@pytest.mark.timeout(900)
+def test_published_hopf_n512_gparareal_k_exact(gpu):
+    """Hopf.py N = 512 GParareal (theta [1, 1], fatol = xatol = 1e-6; the full GP grows to ~9 500
+    training rows, factored by the left-looking 64-column order): K = 19, ~255 s."""
+    out, pk = _run(gpu, 'hopf_512_gp')
+    assert out['converged'] and out['K'] == pk == 19

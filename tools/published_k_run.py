@@ -25,8 +25,22 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, 'tests')]
 import published_k as P   # noqa: E402
 
 
+def heartbeat(period=60):
+    """A line every `period` s while a long native call runs (a GParareal training call at the
+    published scale can take minutes; gpurun kills a command silent for 3 minutes)."""
+    import threading
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(period)
+            print(f'[heartbeat] {time.time() - t0:.0f} s', flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main(names):
     import torch
+    heartbeat()
     import nngp_amd as gpu
     torch.cuda.set_device(0)
     out_dir = os.path.join(ROOT, 'gpurun_out', 'published_k')
