@@ -546,53 +546,6 @@ __device__ __forceinline__ void gpf_ll_factor(double (&a)[LB], int i, int pb, do
     Lb[LB * LB + i] = myr;
 }
 
-// The same factor by a whole 256-thread workgroup on the block in LDS (X, row stride LB + 1): one
-// column per step and a barrier after it; thread (i = tid / 4, q = tid % 4) updates row i's entries
-// k = q, q + 4, ... in (j, i].  l_ij = a_ij * (1/L_jj) and l_kj = a_kj * (1/L_jj) are recomputed from
-// the unscaled column (the same single roundings gpf_ll_factor stores), then a_ik - l_ij l_kj: bitwise
-// gpf_ll_factor's result (NNGP_GPF_FUSE=0 runs that one; tests/test_gpu_gpfull.py compares them).
-// One wave per block (1 152 blocks on 1 024 SIMDs, each column's broadcast and ~130 VALU exposed at
-// one wave per SIMD) took ~40 us per block at Burgers sizes.
-template <bool FMA>
-__device__ __forceinline__ void gpf_ll_factor_wg(double *X, int pb, int b, int32_t *__restrict__ fail,
-                                                 double *__restrict__ Lpan, double *dl) {
-    const int tid = threadIdx.x, i = tid >> 2, q = tid & 3;
-    constexpr int XS = LB + 1;
-    bool bad = false;
-    for (int j = 0; j < pb; j++) {
-        const double djj = X[j * XS + j];
-        bad = bad || !(djj > 0.0);
-        const double ljj = sqrt(djj);
-        const double rj = 1.0 / ljj;
-        if (tid == 0) {
-            dl[j] = ljj;
-            dl[LB + j] = rj;
-        }
-        if (i > j && i < pb) {
-            const double lij = X[i * XS + j] * rj;
-#pragma unroll
-            for (int m = 0; m < LB / 4; m++) {
-                const int k = q + 4 * m;
-                if (k > j && k <= i) X[i * XS + k] = gpf_msub<FMA>(X[i * XS + k], lij, X[k * XS + j] * rj);
-            }
-        }
-        __syncthreads();
-    }
-    if (bad) {
-        if (tid == 0) fail[b] = 1;
-        return;
-    }
-    double *Lb = Lpan + (size_t)b * LPS64;
-    for (int e = tid; e < LB * LB; e += 256) {   // column-major: consecutive threads, consecutive rows
-        const int k = e >> 6, r = e & 63;
-        double v = 0.0;
-        if (r < pb && k < r) v = X[r * XS + k] * dl[LB + k];
-        if (r < pb && k == r) v = dl[r];
-        Lb[e] = v;
-    }
-    if (tid < LB) Lb[LB * LB + tid] = tid < pb ? dl[LB + tid] : 1.0;
-}
-
 // FLY: panel 0, the block's original entries computed (gpf_entry); else read from A (the panel
 // GEMM left them there, NNGP_GPF_FUSE=0)
 template <bool FMA>
@@ -622,36 +575,11 @@ __global__ void __launch_bounds__(64) gpf_ll_diag_kernel(const double *__restric
     gpf_ll_factor<FMA>(a, i, pb, col, b, fail, Lpan);
 }
 
-// Panel 0's diagonal block by a workgroup (gpf_ll_factor_wg), its entries computed into LDS
-template <bool FMA>
-__global__ void __launch_bounds__(256) gpf_ll_diag0_kernel(int n, int pb, int32_t *__restrict__ fail,
-                                                            double *__restrict__ Lpan, int nmat,
-                                                            const double *__restrict__ D2,
-                                                            const double *__restrict__ Y, int d,
-                                                            const GPPoint *__restrict__ pts) {
-    const int b = blockIdx.x;
-    if (b >= nmat || fail[b]) return;
-    __shared__ double X[LB * (LB + 1)];
-    __shared__ double dl[2 * LB];
-    const GPPoint pt = pts[b];
-    double v[LB * LB / 256];
-#pragma unroll
-    for (int u = 0; u < LB * LB / 256; u++) {   // all entries first, clamped (no branch around a load)
-        const int e = threadIdx.x + 256 * u, r = e >> 6, k = e & 63;
-        v[u] = gpf_entry(D2, n, Y, d, pt, min(r, pb - 1), min(k, pb - 1));
-    }
-#pragma unroll
-    for (int u = 0; u < LB * LB / 256; u++) {
-        const int e = threadIdx.x + 256 * u, r = e >> 6, k = e & 63;
-        X[r * (LB + 1) + k] = (r < pb && k <= r) ? v[u] : 0.0;
-    }
-    __syncthreads();
-    gpf_ll_factor_wg<FMA>(X, pb, b, fail, Lpan, dl);
-}
-
 // FUSED: the diagonal tile's workgroup (dispatched before the matrix's other tiles: gpf_xcd_map
-// gives tile 0 the matrix's lowest linear id) leaves its updated block in LDS and factors it with
-// all four waves (gpf_ll_factor_wg, bitwise gpf_ll_diag_kernel's result), one launch fewer per panel
+// gives tile 0 the matrix's lowest linear id) leaves its updated block in LDS and factors it on
+// wave 0 -- gpf_ll_diag_kernel's arithmetic on the same values, one launch fewer per panel.  (The
+// factor on all four waves, a barrier per column, and the row solve reading L11 by scalar loads
+// were both measured slower at Burgers sizes and removed: DESIGN.md §8.)
 template <bool FUSED, bool FMA>
 __global__ void __launch_bounds__(256, 2) gpf_ll_gemm_kernel(double *__restrict__ A, int n, int c0, int pb,
                                                               int32_t *__restrict__ fail, double *__restrict__ Lpan,
@@ -678,9 +606,14 @@ __global__ void __launch_bounds__(256, 2) gpf_ll_gemm_kernel(double *__restrict_
     }
     if constexpr (FUSED) {
         if (t != 0) return;
-        __shared__ double dl[2 * LB];
         __syncthreads();
-        gpf_ll_factor_wg<FMA>(Xd, pb, b, fail, Lpan, dl);
+        if (threadIdx.x >= 64) return;
+        __shared__ __attribute__((aligned(16))) double col[LB];
+        const int i = threadIdx.x;
+        double a[LB];
+#pragma unroll
+        for (int k = 0; k < LB; k++) a[k] = (i < pb && k <= i) ? Xd[i * (LB + 1) + k] : 0.0;
+        gpf_ll_factor<FMA>(a, i, pb, col, b, fail, Lpan);
     }
 }
 
@@ -734,12 +667,13 @@ __global__ void __launch_bounds__(256) gpf_ll_rows_kernel(double *__restrict__ A
 #pragma unroll
         for (int u = 0; u < NL; u++)
             if (tid + 256 * u < LPS64) L[tid + 256 * u] = lv[u];
+        __syncthreads();
     }
-    __syncthreads();
+    const double *Lr = L;
     if (t == 0)   // L11 into A's diagonal block, coalesced along the rows
         for (int e = tid; e < LB * LB; e += 256) {
             const int ii = e >> 6, k = e & 63;
-            if (k <= ii && ii < pb) Ab[(size_t)(c0 + ii) * ld + c0 + k] = L[k * LB + ii];
+            if (k <= ii && ii < pb) Ab[(size_t)(c0 + ii) * ld + c0 + k] = Lr[k * LB + ii];
         }
     if (!act) return;                            // (no barrier follows)
     double x[LB];
@@ -764,9 +698,9 @@ __global__ void __launch_bounds__(256) gpf_ll_rows_kernel(double *__restrict__ A
 #pragma unroll
     for (int j = 0; j < LB; j++) {
         if (j < pb) {
-            x[j] = x[j] * L[LB * LB + j];
+            x[j] = x[j] * Lr[LB * LB + j];
 #pragma unroll
-            for (int k = j + 1; k < LB; k++) x[k] = gpf_msub<FMA>(x[k], x[j], L[j * LB + k]);
+            for (int k = j + 1; k < LB; k++) x[k] = gpf_msub<FMA>(x[k], x[j], Lr[j * LB + k]);
         }
     }
 #pragma unroll
@@ -929,13 +863,6 @@ static int gpf_eval(const double *D2, int n, const double *Y, int d, const GPPoi
                 else
                     hipLaunchKernelGGL((gpf_ll_gemm_kernel<true, false>), gg, dim3(256), 0, st, A, n, c0, pb, fail,
                                        Lpan, T, nb, D2, Y, d, pts);
-            } else if (c0 == 0 && fused) {   // panel 0: no GEMM; its block factored by a workgroup
-                if (fma)
-                    hipLaunchKernelGGL(gpf_ll_diag0_kernel<true>, dim3(nb), dim3(256), 0, st, n, pb, fail, Lpan, nb, D2,
-                                       Y, d, pts);
-                else
-                    hipLaunchKernelGGL(gpf_ll_diag0_kernel<false>, dim3(nb), dim3(256), 0, st, n, pb, fail, Lpan, nb,
-                                       D2, Y, d, pts);
             } else {
                 if (c0 > 0)
                     hipLaunchKernelGGL((gpf_ll_gemm_kernel<false, false>), gg, dim3(256), 0, st, A, n, c0, pb, fail,
@@ -948,12 +875,13 @@ static int gpf_eval(const double *D2, int n, const double *Y, int d, const GPPoi
                                        nb, D2, Y, d, pts);
             }
             const int TR = (n + 1 - c0 - pb + 255) / 256;   // >= 1: row n is always below
+            const dim3 gr((unsigned)TR, ny8);
             if (fma)
-                hipLaunchKernelGGL(gpf_ll_rows_kernel<true>, dim3(TR, ny8), dim3(256), 0, st, A, n, c0, pb, fail, Lpan,
-                                   TR, nb, D2, Y, d, pts);
+                hipLaunchKernelGGL(gpf_ll_rows_kernel<true>, gr, dim3(256), 0, st, A, n, c0, pb, fail, Lpan, TR, nb, D2, Y,
+                                   d, pts);
             else
-                hipLaunchKernelGGL(gpf_ll_rows_kernel<false>, dim3(TR, ny8), dim3(256), 0, st, A, n, c0, pb, fail,
-                                   Lpan, TR, nb, D2, Y, d, pts);
+                hipLaunchKernelGGL(gpf_ll_rows_kernel<false>, gr, dim3(256), 0, st, A, n, c0, pb, fail, Lpan, TR, nb, D2,
+                                   Y, d, pts);
         }
     } else {
         for (int p0 = 0; p0 < n; p0 += GPB) {

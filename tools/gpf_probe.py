@@ -20,8 +20,9 @@ import nngp_amd as g  # noqa: E402
 from nngp_amd import _lib  # noqa: E402
 
 SHAPES = [(753, 1152), (378, 1152), (2048, 27), (4096, 240), (9500, 27)]
-ORDERS = [('ll64', {'NNGP_GPF_ORDER': '0', 'NNGP_GPF_FMA': '0'}),
-          ('ll64_fma', {'NNGP_GPF_ORDER': '0', 'NNGP_GPF_FMA': '1'}),
+ORDERS = [('ll64', {'NNGP_GPF_ORDER': '0', 'NNGP_GPF_FMA': '0', 'NNGP_GPF_FUSE': '1'}),
+          ('ll64_unfused', {'NNGP_GPF_ORDER': '0', 'NNGP_GPF_FMA': '0', 'NNGP_GPF_FUSE': '0'}),
+          ('ll64_fma', {'NNGP_GPF_ORDER': '0', 'NNGP_GPF_FMA': '1', 'NNGP_GPF_FUSE': '1'}),
           ('rl32', {'NNGP_GPF_ORDER': '1', 'NNGP_GPF_FMA': '0'})]
 
 
