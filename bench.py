@@ -262,14 +262,24 @@ def published_k_table(torch, g, live_extra=None):
                       'wall_s': time.perf_counter() - t0, 'source': 'live', 'schedule': 'unpaged'}
     for name, v in (live_extra or {}).items():
         rows[name] = dict(v, source='live')
+    # every round's recorded rows, the newest round's file winning per name; runs stopped at a
+    # session deadline (<name>.partial.json, tools/published_k_run.py) are listed apart, not counted
     dirs = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r[0-9]*', 'published_k')))
-    if dirs:
-        for f in sorted(glob.glob(os.path.join(dirs[-1], '*.json'))):
+    partial = {}
+    for dr in reversed(dirs):
+        for f in sorted(glob.glob(os.path.join(dr, '*.json'))):
             name = os.path.basename(f)[:-5]
-            if name in rows or '@' in name:   # name@seed: the seed-spread runs
+            if '@' in name:   # name@seed: the seed-spread runs
                 continue
             with open(f) as fh:
                 d = json.load(fh)
+            if name.endswith('.partial'):
+                partial.setdefault(name[:-8], {'K_so_far': d['K'], 'converged': d['converged'],
+                                              'published_K': d['published_K'], 'wall_s': d['wall_s'],
+                                              'source': os.path.relpath(f, ROOT)})
+                continue
+            if name in rows:
+                continue
             rows[name] = {'K': d['K'], 'published_K': d['published_K'], 'match': d['K'] == d['published_K'],
                           'wall_s': d['wall_s'], 'source': os.path.relpath(f, ROOT),
                           'schedule': 'paged' if name.endswith('_paged') else 'unpaged'}
@@ -277,7 +287,8 @@ def published_k_table(torch, g, live_extra=None):
     live = [n for n in rows if rows[n]['source'] == 'live']
     rec = [n for n in rows if rows[n]['source'] != 'live']
     cnt = lambda names: f"{sum(rows[n]['match'] for n in names)}/{len(names)}"
-    return {'rows': rows, 'parareal_exact': cnt(det), 'exact_live': cnt(live), 'exact_recorded': cnt(rec),
+    return {'rows': rows, 'partial_runs': partial, 'parareal_exact': cnt(det), 'exact_live': cnt(live),
+            'exact_recorded': cnt(rec), 'exact_all': cnt(list(rows)),
             'note': 'name = <system>_<N>_<model>[_paged]; unpaged = Nf/N RK steps per slice; paged = the '
                     'published scripts\' RK_thresh schedule (every one of 25 / 200 pages re-uses all Nf/N '
                     'steps: a 25x / 200x finer fine step). FHN-PDE d_x = 10 / 12 get 26 pages (float page '
