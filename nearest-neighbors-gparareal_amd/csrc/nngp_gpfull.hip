@@ -416,8 +416,8 @@ __device__ __forceinline__ void gpf_xcd_map(int lin, int T, int &b, int &t) {
 // the factor read it back.  r, c must be inside the matrix (callers clamp).
 __device__ __forceinline__ double gpf_entry(const double *__restrict__ D2, int n, const double *__restrict__ Y, int d,
                                             const GPPoint &p, int r, int c) {
-    const double dv = D2[(size_t)min(r, n - 1) * n + c];   // both loads unconditional (no branch per entry)
-    const double yv = Y[(size_t)c * d + p.coord];
+    const double dv = D2[(unsigned)(min(r, n - 1) * n + c)];   // both loads unconditional (no branch per entry)
+    const double yv = Y[(unsigned)(c * d + p.coord)];
     double v = p.psy * exp(p.c * dv);
     v = (r == c) ? v + p.jp : v;
     return (r == n) ? yv : v;
@@ -446,8 +446,8 @@ __device__ __forceinline__ void gpf_ll_gemm_tile(double *__restrict__ Ab, int ld
     _Pragma("unroll") for (int u = 0; u < SU; u++) {                                                   \
         const int rr = sr + RS * u;                                                                    \
         const int ra = FULL ? r0 + rr : min(r0 + rr, n), rb = FULL ? rr : min(rr, pb - 1);             \
-        const double x = Ab[(size_t)ra * ld + (kk) + sk];                                              \
-        const double y = DIAG ? 0.0 : Ab[(size_t)(c0 + rb) * ld + (kk) + sk];                          \
+        const double x = Ab[(unsigned)(ra * ld + (kk) + sk)];                                          \
+        const double y = DIAG ? 0.0 : Ab[(unsigned)((c0 + rb) * ld + (kk) + sk)];                      \
         va[u] = (FULL || r0 + rr <= n) ? x : 0.0;                                                      \
         vb[u] = (FULL || rr < pb) ? y : 0.0;                                                           \
     }
@@ -474,30 +474,28 @@ __device__ __forceinline__ void gpf_ll_gemm_tile(double *__restrict__ Ab, int ld
                 acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, SB[(16 * cb + cl) * LKS + k + kq], acc[cb], 0, 0, 0);
         }
     }
-    // the original entries of this tile's panel columns, all computed before any store
-    double ov[4][4];
+    if (Xd) __syncthreads();                  // the last chunk's operand reads are done: Xd reuses their LDS
+    // the original entries of this tile's panel columns (computed, not read), one row group at a time
+    // (a group's four entries are loaded and computed before its stores; all sixteen at once held 32
+    // more VGPRs through the epilogue)
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int i = 16 * w + kq + 4 * r;
+        double ov[4];
 #pragma unroll
         for (int cb = 0; cb < 4; cb++) {
             const int j = 16 * cb + cl;
-            ov[cb][r] = gpf_entry(D2, n, Y, d, pt, FULL ? r0 + i : min(r0 + i, n), c0 + (FULL ? j : min(j, pb - 1)));
+            ov[cb] = gpf_entry(D2, n, Y, d, pt, FULL ? r0 + i : min(r0 + i, n), c0 + (FULL ? j : min(j, pb - 1)));
         }
-    }
-    if (Xd) __syncthreads();                  // the last chunk's operand reads are done: Xd reuses their LDS
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const int i = 16 * w + kq + 4 * r;
 #pragma unroll
         for (int cb = 0; cb < 4; cb++) {
             const int j = 16 * cb + cl;
             if ((FULL || (r0 + i <= n && j < pb)) && (!DIAG || j <= i)) {
-                const double v = ov[cb][r] - acc[cb][r];
+                const double v = ov[cb] - acc[cb][r];
                 // the fused diagonal factor's input stays in LDS; the rows below it in tile 0 (the
                 // last, short panel: row n) go to A for the row solve
                 if (Xd && i < pb) Xd[i * (LB + 1) + j] = v;
-                else Ab[(size_t)(r0 + i) * ld + c0 + j] = v;
+                else Ab[(unsigned)((r0 + i) * ld + c0 + j)] = v;
             }
         }
     }
@@ -581,7 +579,7 @@ __global__ void __launch_bounds__(64) gpf_ll_diag_kernel(const double *__restric
 // factor on all four waves, a barrier per column, and the row solve reading L11 by scalar loads
 // were both measured slower at Burgers sizes and removed: DESIGN.md §8.)
 template <bool FUSED, bool FMA>
-__global__ void __launch_bounds__(256, 2) gpf_ll_gemm_kernel(double *__restrict__ A, int n, int c0, int pb,
+__global__ void __launch_bounds__(256, FUSED ? 2 : 4) gpf_ll_gemm_kernel(double *__restrict__ A, int n, int c0, int pb,
                                                               int32_t *__restrict__ fail, double *__restrict__ Lpan,
                                                               int T, int nmat, const double *__restrict__ D2,
                                                               const double *__restrict__ Y, int d,
@@ -943,7 +941,10 @@ static int gpf_workspace(int n, int nb, GPFWork &w) {
 }
 
 static int gpf_check(int64_t rows, int d, int n_fit) {
-    NNGP_REQUIRE(rows >= 1 && rows <= (int64_t)1 << 30, "full GP needs 1 <= rows (got %lld)", (long long)rows);
+    // (rows+1)^2 and rows*d index in 32 bits inside the left-looking kernels (32-bit offsets from a
+    // uniform base let the loads use scalar bases: fewer VGPRs, 4 workgroups per CU)
+    NNGP_REQUIRE(rows >= 1 && rows <= 46000, "full GP needs 1 <= rows <= 46000 (got %lld)", (long long)rows);
+    NNGP_REQUIRE((int64_t)rows * d < ((int64_t)1 << 31), "full GP: rows x d too large");
     NNGP_REQUIRE(d >= 1 && n_fit >= 1, "bad d / fit count");
     return NNGP_OK;
 }
