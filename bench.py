@@ -540,6 +540,41 @@ def gparareal_burgers(torch, g):
             'frac_fp64_peak_executed': ex / max(sum(train), 1e-9) / 1e12 / FP64_PEAK_TFLOPS}
 
 
+def gpfull_round_roofline(torch, g, shapes=((4096, 240), (9500, 27), (753, 1152)), reps=3):
+    """One batched full-GP -LML evaluation = one GParareal Nelder-Mead round (nngp_gpfull_lml:
+    the left-looking 64-column Cholesky of every point's (rows+1)^2 matrix) at the
+    shapes the published runs reach -- FHN-PDE d_x = 10 (240 of its 1 800 matrices per slab),
+    Hopf N = 512, Burgers N = 128 -- with a jitter that lets every factor complete, so the executed
+    flops are exactly points x (rows+1)^3 / 3 (bound: the FP64 matrix cores, 78.6 TF/s)."""
+    import ctypes
+    out = {}
+    ip, dp = ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)
+    for n, npts in shapes:
+        rng = np.random.default_rng(n)
+        x = rng.uniform(-1, 1, (n, 3))
+        X = torch.tensor(x, device='cuda')
+        Y = torch.tensor(np.sin(2 * x), device='cuda')
+        c = np.ascontiguousarray(np.arange(npts) % 3, dtype=np.int32)
+        jx = np.full(npts, -2.0)
+        th = np.ascontiguousarray(np.column_stack([0.3 + 0.5 * rng.random(npts), 0.5 + rng.random(npts)]))
+        fv = np.empty(npts)
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            g._lib.check(g.lib().nngp_gpfull_lml(X.data_ptr(), n, 3, Y.data_ptr(), npts, c.ctypes.data_as(ip),
+                                                 jx.ctypes.data_as(dp), th.ctypes.data_as(dp), fv.ctypes.data_as(dp),
+                                                 None, None))
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        t = min(ts)
+        fl = npts * (n + 1) ** 3 / 3
+        out[f'{n}x{npts}'] = {'ms': t * 1e3, 'tflops': fl / t / 1e12, 'frac_fp64_peak': fl / t / 1e12 / FP64_PEAK_TFLOPS,
+                              'all_finite': bool(np.isfinite(fv).all())}
+    log('gpfull round roofline', json.dumps(out))
+    return out
+
+
 def _oracle():
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import oracle as O
@@ -1107,6 +1142,7 @@ def main():
                                                                          'tomlab_n256_configs_schedule_nngp')}))
         res['gparareal_lorenz_n32'] = gparareal_lorenz(torch, g)
         res['gparareal_burgers_n128'] = gparareal_burgers(torch, g)
+        res['gparareal_round_roofline'] = gpfull_round_roofline(torch, g)
         log('gparareal burgers', json.dumps(res['gparareal_burgers_n128']))
         log('gparareal lorenz K', res['gparareal_lorenz_n32']['K'], f"{res['gparareal_lorenz_n32']['wall_s']:.2f}s")
         res['burgers_n128_published_schedule'] = burgers_published_schedule(torch, g)
