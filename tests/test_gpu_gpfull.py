@@ -208,3 +208,24 @@ def test_gparareal_checkpoint_resume_is_bitwise(gpu, tmp_path):
     res = p.load_int_dump(str(tmp_path / 'gp' / 'gp_2.npz'), early_stop=6)
     assert res['k'] == full['k'] and res['conv_int'] == full['conv_int']
     assert np.array_equal(np.nan_to_num(res['u'], nan=7.0), np.nan_to_num(full['u'], nan=7.0))
+
+
+def test_gpfull_fit_chunked_slab_is_bitwise(gpu, monkeypatch):
+    """nngp_gpfull_fit with the Nelder-Mead rounds' points factored in several slab chunks
+    (NNGP_GPF_SLAB_MB below one round's matrices, as FHN-PDE d_x = 10 at published scale needs)
+    returns the same fits, bit for bit, as one slab: chunking only groups independent factors."""
+    import torch
+    rng = np.random.default_rng(7)
+    n, d = 300, 4
+    x = rng.uniform(-1, 1, (n, d))
+    y = np.sin(2 * x) + 0.01 * rng.standard_normal((n, d))
+    m = gpu.GPjax_p(n=d, N=32)
+    X, Y = _dev(torch, x), _dev(torch, y)
+    coords = [j for j in range(d) for _ in range(9)]
+    jit = [float(v) for _ in range(d) for v in range(-20, -11)]
+    th0 = [(1.0, 1.0)] * len(coords)
+    a = m._fit_batch(X, Y, coords, jit, th0)
+    monkeypatch.setenv('NNGP_GPF_SLAB_MB', '3')   # 4 matrices of 301^2 per chunk: 9 chunks per round
+    b = m._fit_batch(X, Y, coords, jit, th0)
+    for u, v in zip(a, b):
+        assert np.array_equal(np.nan_to_num(u, nan=7.0), np.nan_to_num(v, nan=7.0))

@@ -60,6 +60,8 @@ def main(names):
             extra.update(store_int=True, int_dir=ckpt, int_name=tag)
         if budget > 0:
             extra['stop_at'] = t0 + budget
+        if os.environ.get('NNGP_PK_EARLY_STOP'):   # a diagnostic prefix of the run
+            extra['early_stop'] = int(os.environ['NNGP_PK_EARLY_STOP'])
         dumps = sorted(glob.glob(os.path.join(ckpt, tag, f'{tag}_*.npz')),
                        key=lambda f: int(f.rsplit('_', 1)[1][:-4])) if ckpt else []
         if dumps:
@@ -74,8 +76,10 @@ def main(names):
         if dumps:
             summ['resumed_from'] = os.path.basename(dumps[-1])
             summ['runtime_s_incl_earlier_sessions'] = summ['runtime_s']
-        if not r['converged'] and budget > 0 and r['k'] < s.N:
+        if not r['converged'] and (budget > 0 or 'early_stop' in extra) and r['k'] < s.N:
             tag = tag + '.partial'
+        if os.environ.get('NNGP_PK_TAG'):
+            tag = tag + '.' + os.environ['NNGP_PK_TAG']
         with open(os.path.join(out_dir, tag + '.json'), 'w') as f:
             json.dump(summ, f, indent=1)
         print('RESULT', json.dumps(summ), flush=True)
