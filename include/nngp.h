@@ -236,12 +236,13 @@ int64_t nngp_sweep_late_reruns(void);
 int nngp_shutdown(void);
 
 /* ---- 4. full-data GParareal (models.GPjax_p, models.py:273-473) ------------------------------
- * The training set X, Y: DEVICE [rows][d], rows >= 1 (no fixed limit: the scratch is rows^2
- * doubles for D^2 plus (rows+1)^2 per point factored together, batched to <= 8 GB but at least one
- * point, so device memory bounds rows, ~1e5 on a 288 GB MI355X; up to 7 936 rows the alpha solve
- * keeps its vector in LDS, past that in its output row).  K = sigma_y^2 exp(-0.5/sigma_x^2 D^2)
- * + 10^jitter I over ALL rows (kernel_np / _fit_gp_np, models.py:300-312), theta = (sigma_x,
- * sigma_y) in linear units.  Points and fits are batched: one blocked Cholesky per point.
+ * The training set X, Y: DEVICE [rows][d], 1 <= rows <= 46 000 (32-bit offsets inside a matrix;
+ * the scratch is rows^2 doubles for D^2 plus (rows+1)^2 per point factored together, in slabs of
+ * <= NNGP_GPF_SLAB_MB, default 32 GB, but at least one point; up to 7 936 rows the alpha solve
+ * keeps its vector in LDS, past that in its output row).  The factor is a left-looking Cholesky
+ * on 64-column panels.  K = sigma_y^2 exp(-0.5/sigma_x^2 D^2) + 10^jitter I over
+ * ALL rows (kernel_np / _fit_gp_np, models.py:300-312), theta = (sigma_x, sigma_y) in linear
+ * units.  Points and fits are batched: one blocked Cholesky per point.
  *
  * nngp_gpfull_lml: -LML of n_pts points (GPjax_p.log_lik, models.py:321-327; +inf when the
  * Cholesky fails).  coord, jitter_exp, theta [n_pts][2], fval_out: HOST.  alpha_out: DEVICE
