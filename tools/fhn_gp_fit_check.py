@@ -7,6 +7,9 @@ numpy/LAPACK Cholesky + scipy Nelder-Mead, the reference's own algorithm) on the
 import json
 import os
 import sys
+
+os.environ.setdefault('OMP_NUM_THREADS', '1')       # one BLAS thread per worker process
+os.environ.setdefault('OPENBLAS_NUM_THREADS', '1')
 from concurrent.futures import ProcessPoolExecutor
 
 import numpy as np
@@ -20,6 +23,7 @@ from nngp_amd.models import JITTERS, _select_fit  # noqa: E402
 def coord_fits(args):
     x, y, j = args
     out = [GF.gp_fit(x, y, np.array([1.0, 1.0]), jit, 1e-4, 1e-4) for jit in JITTERS]
+    print(f'coord {j} done', flush=True)
     th = np.array([o[0] for o in out])
     fv = np.array([o[1] for o in out])
     return j, th, fv, [o[2] for o in out]
